@@ -1,0 +1,248 @@
+"""consus_amd -- MI355X-native CRC-32C engine for Consus's durable-log path.
+
+Python mirror of the reference operator interface (``consus::crc32c``,
+common/crc32c.h:40-41) over the C ABI of ``include/consus_crc32c.h``
+(``consus_amd/lib/libconsus_crc32c.so``).  Every checksum is computed by the
+HIP kernels; if the library or a gfx950 device is missing, calls raise
+``EngineError`` -- there is no CPU fallback.
+
+    from consus_amd import crc32c, crc32c_batch
+    crc32c(0, b"123456789")            # -> 0xE3069283, same as consus::crc32c
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libconsus_crc32c.so")
+REPO = os.path.dirname(HERE)
+HEADERS = [os.path.join(REPO, "include", "consus_crc32c.h"),
+           os.path.join(REPO, "include", "consus_durable_log.h")]
+
+OK = 0
+EINVAL = -22
+ENODEV = -19
+ENOMEM = -12
+EHIP = -5
+ERCCL = -71
+FLAG_DEVICE = 0x1
+FLAG_ASYNC = 0x2
+MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D = 1, 2, 3
+
+
+class EngineError(RuntimeError):
+    def __init__(self, status: int, what: str, detail: str = ""):
+        self.status = status
+        super().__init__(f"{what} failed with status {status}: {detail}")
+
+
+def build() -> None:
+    """Compile libconsus_crc32c.so for gfx950 in-tree (hipcc)."""
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(HERE, "csrc")], check=True)
+
+
+_u8p = C.c_void_p
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+
+_SIGS = {
+    "mi_crc32c_init": (C.c_int, [C.c_int]),
+    "mi_crc32c_strerror": (C.c_char_p, [C.c_int]),
+    "mi_crc32c_last_error": (C.c_char_p, []),
+    "mi_crc32c_stream": (C.c_void_p, []),
+    "mi_crc32c_stream_sync": (C.c_int, []),
+    "mi_crc32c": (C.c_uint32, [C.c_uint32, C.c_void_p, C.c_size_t]),
+    "mi_crc32c_buffer": (C.c_int, [C.c_uint32, C.c_void_p, C.c_size_t, _u32p, C.c_uint]),
+    "mi_crc32c_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                  C.c_uint64, C.c_void_p, C.c_uint]),
+    "mi_crc32c_batch_fixed": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                        C.c_size_t, C.c_void_p, C.c_uint]),
+    "mi_crc32c_combine": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint64]),
+    "mi_crc32c_combine_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                          C.c_void_p, C.c_uint]),
+    "mi_crc32c_pipeline_create": (C.c_int, [C.c_size_t, C.c_size_t, C.c_int,
+                                            C.POINTER(C.c_void_p)]),
+    "mi_crc32c_pipeline_submit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                            C.POINTER(C.c_uint64)]),
+    "mi_crc32c_pipeline_wait": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "mi_crc32c_pipeline_destroy": (C.c_int, [C.c_void_p]),
+    "mi_dev_malloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
+    "mi_dev_free": (C.c_int, [C.c_void_p]),
+    "mi_host_malloc_pinned": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
+    "mi_host_free_pinned": (C.c_int, [C.c_void_p]),
+    "mi_memcpy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
+    "mi_memset": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t]),
+    "mi_fill_splitmix64": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint64]),
+    "mi_timer_start": (C.c_int, []),
+    "mi_timer_stop": (C.c_int, [C.POINTER(C.c_float)]),
+    "mi_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "mi_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "mi_comm_allgather_u32": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
+    "mi_comm_destroy": (C.c_int, []),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the engine library (raises EngineError if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(ENODEV, "load", f"{LIB_PATH} missing: run consus_amd.build()")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(status: int, what: str) -> None:
+    if status != OK:
+        detail = (lib().mi_crc32c_last_error() or b"").decode(errors="replace")
+        raise EngineError(status, what, detail)
+
+
+def _np_ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(data), dtype=np.uint8)
+    return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+
+
+def init(device: int = 0) -> None:
+    _check(lib().mi_crc32c_init(device), "mi_crc32c_init")
+
+
+# ---- the reference operator -------------------------------------------------
+def crc32c(init_crc: int, data, n: int | None = None) -> int:
+    """consus::crc32c(init, data, n) (common/crc32c.cc:122-126), on the GPU."""
+    a = _as_u8(data)
+    n = a.size if n is None else n
+    if n > a.size:
+        raise ValueError("n exceeds buffer")
+    out = C.c_uint32(0)
+    _check(lib().mi_crc32c_buffer(init_crc & 0xFFFFFFFF, C.c_void_p(a.ctypes.data), n,
+                                  C.byref(out), 0), "mi_crc32c_buffer")
+    return int(out.value)
+
+
+def crc32c_batch(buf, offsets, lengths, inits=None) -> np.ndarray:
+    """Per-record CRCs of host records [buf + off, +len)."""
+    a = _as_u8(buf)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if off.size != ln.size:
+        raise ValueError("offsets/lengths size mismatch")
+    if off.size and int((off + ln.astype(np.uint64)).max()) > a.size:
+        raise ValueError("record outside buffer")
+    ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+    out = np.zeros(off.size, dtype=np.uint32)
+    _check(lib().mi_crc32c_batch(C.c_void_p(a.ctypes.data), _np_ptr(off), _np_ptr(ln),
+                                 _np_ptr(ini), off.size, int(ln.sum(dtype=np.uint64)),
+                                 _np_ptr(out), 0), "mi_crc32c_batch")
+    return out
+
+
+def crc32c_fixed(buf, stride: int, length: int, count: int, inits=None) -> np.ndarray:
+    a = _as_u8(buf)
+    if count and (count - 1) * stride + length > a.size:
+        raise ValueError("records outside buffer")
+    ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+    out = np.zeros(count, dtype=np.uint32)
+    _check(lib().mi_crc32c_batch_fixed(C.c_void_p(a.ctypes.data), stride, length, _np_ptr(ini),
+                                       count, _np_ptr(out), 0), "mi_crc32c_batch_fixed")
+    return out
+
+
+def combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    return int(lib().mi_crc32c_combine(crc_a, crc_b, len_b))
+
+
+# ---- device-resident buffers ----------------------------------------------------
+class DeviceBuffer:
+    """A device allocation owned by Python (hipMalloc through the engine)."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p(0)
+        _check(lib().mi_dev_malloc(C.byref(p), max(int(nbytes), 1)), "mi_dev_malloc")
+        self.ptr = int(p.value)
+        self.nbytes = int(nbytes)
+
+    def free(self) -> None:
+        if self.ptr:
+            _check(lib().mi_dev_free(C.c_void_p(self.ptr)), "mi_dev_free")
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def upload(self, arr, offset: int = 0) -> None:
+        a = np.ascontiguousarray(arr)
+        if offset + a.nbytes > self.nbytes:
+            raise ValueError("upload overflows buffer")
+        _check(lib().mi_memcpy(C.c_void_p(self.ptr + offset), C.c_void_p(a.ctypes.data), a.nbytes,
+                               MEMCPY_H2D), "mi_memcpy")
+
+    def download(self, dtype=np.uint8, count: int | None = None, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = (self.nbytes - offset) // dt.itemsize if count is None else count
+        out = np.empty(n, dtype=dt)
+        _check(lib().mi_memcpy(C.c_void_p(out.ctypes.data), C.c_void_p(self.ptr + offset),
+                               out.nbytes, MEMCPY_D2H), "mi_memcpy")
+        return out
+
+    def fill_splitmix64(self, seed: int, byte_offset: int = 0, nbytes: int | None = None,
+                        dst_offset: int = 0) -> None:
+        n = self.nbytes - dst_offset if nbytes is None else nbytes
+        _check(lib().mi_fill_splitmix64(C.c_void_p(self.ptr + dst_offset), n, seed, byte_offset),
+               "mi_fill_splitmix64")
+
+    def memset(self, value: int = 0) -> None:
+        _check(lib().mi_memset(C.c_void_p(self.ptr), value, self.nbytes), "mi_memset")
+
+
+def device_batch_fixed(data: DeviceBuffer, stride: int, length: int, count: int,
+                       out: DeviceBuffer, inits: DeviceBuffer | None = None,
+                       asynchronous: bool = False, data_offset: int = 0) -> None:
+    flags = FLAG_DEVICE | (FLAG_ASYNC if asynchronous else 0)
+    _check(lib().mi_crc32c_batch_fixed(C.c_void_p(data.ptr + data_offset), stride, length,
+                                       None if inits is None else C.c_void_p(inits.ptr), count,
+                                       C.c_void_p(out.ptr), flags), "mi_crc32c_batch_fixed")
+
+
+def device_batch(data: DeviceBuffer, offsets: DeviceBuffer, lengths: DeviceBuffer, count: int,
+                 out: DeviceBuffer, inits: DeviceBuffer | None = None, total_bytes: int = 0,
+                 asynchronous: bool = False) -> None:
+    flags = FLAG_DEVICE | (FLAG_ASYNC if asynchronous else 0)
+    _check(lib().mi_crc32c_batch(C.c_void_p(data.ptr), C.c_void_p(offsets.ptr),
+                                 C.c_void_p(lengths.ptr),
+                                 None if inits is None else C.c_void_p(inits.ptr), count,
+                                 total_bytes, C.c_void_p(out.ptr), flags), "mi_crc32c_batch")
+
+
+def sync() -> None:
+    _check(lib().mi_crc32c_stream_sync(), "mi_crc32c_stream_sync")
+
+
+def timer_start() -> None:
+    _check(lib().mi_timer_start(), "mi_timer_start")
+
+
+def timer_stop() -> float:
+    ms = C.c_float(0)
+    _check(lib().mi_timer_stop(C.byref(ms)), "mi_timer_stop")
+    return float(ms.value)

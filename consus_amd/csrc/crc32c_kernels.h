@@ -1,0 +1,87 @@
+// consus_amd/csrc/crc32c_kernels.h -- launch interface of the CDNA4 kernels.
+//
+// Internal to libconsus_crc32c.so; the public boundary is include/consus_crc32c.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mi_crc {
+
+// Geometry of the record kernels.
+constexpr int kTeam = 8;                    // lanes per record ("team")
+constexpr int kRowBytes = 16 * kTeam;       // one row = 16 B per lane = 128 B
+constexpr int kGroupRows = 8;               // rows per software-pipelined group
+constexpr int kGroupBytes = kRowBytes * kGroupRows;  // 1 KiB
+constexpr int kChunk = 4096;                // variable-length work unit
+constexpr int kBlock = 1024;                // threads per workgroup (16 waves)
+constexpr int kSmallRecord = 32;            // records shorter than this are finished byte-serially
+
+// Global table image uploaded once per device (u32 words).
+constexpr int kTabMain = 0;                 // G^{128}_j, 4 x 256  (row fold, replicated bank-private in LDS)
+constexpr int kTabT = 1024;                 // T_0..T_15, 16 x 256 (slice-by-16)
+constexpr int kTabZ32 = kTabT + 4096;       // G^{32}_j
+constexpr int kTabZ64 = kTabZ32 + 1024;     // G^{64}_j
+constexpr int kTabZChunk = kTabZ64 + 1024;  // G^{4096}_j (chunk combine)
+constexpr int kTabZero = kTabZChunk + 1024;  // 4 zero words (init 0 when inits == nullptr)
+constexpr int kTabWords = kTabZero + 4;
+
+// LDS image of the record kernels (bytes).
+constexpr uint32_t kLdsMain = 0;            // 128 KiB bank-private G^{128}
+constexpr uint32_t kLdsT = 131072;          // 16 KiB
+constexpr uint32_t kLdsZ32 = kLdsT + 16384;
+constexpr uint32_t kLdsZ64 = kLdsZ32 + 4096;
+constexpr uint32_t kLdsBytes = kLdsZ64 + 4096;  // 155648
+
+// One unit of variable-length work: the bytes [end - len, end) of a record,
+// end 16-byte aligned.  rec_flag = record index | kItemStart if the chunk
+// holds any of the record's first 4 bytes (the init is folded in there).
+struct Item
+{
+    uint64_t end;
+    uint32_t len;
+    uint32_t rec_flag;
+};
+constexpr uint32_t kItemStart = 0x80000000u;
+// Item::len = bytes (<= kChunk) | (chunk start - record start) << kItemShiftBit
+constexpr uint32_t kItemShiftBit = 16;
+constexpr uint32_t kItemLenMask = 0xFFFFu;
+
+hipError_t configure_kernels();
+
+hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const uint32_t* inits,
+                        uint64_t count, uint32_t* out, const uint32_t* tables, int grid,
+                        hipStream_t stream);
+
+// Variable-length pipeline.  `ws_*` are engine-owned device workspaces.
+struct VarWorkspace
+{
+    uint32_t* blk;        // 4 * nblocks + 4 u32 (bin counts -> offsets, then totals)
+    Item* items;          // capacity `item_cap`
+    uint32_t* partial;    // capacity `item_cap`
+    uint32_t* full_pos;   // count
+    uint32_t* head_pos;   // count
+    uint64_t item_cap;
+};
+
+hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                           uint64_t count, const VarWorkspace& ws, hipStream_t stream);
+hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
+                             const uint32_t* tables, int grid, hipStream_t stream);
+hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                               const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
+                               uint32_t* out, const uint32_t* tables, hipStream_t stream);
+uint32_t var_plan_blocks(uint64_t count);
+
+hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,
+                          uint64_t count, uint32_t* out, const uint32_t* pow2_tables,
+                          hipStream_t stream);
+
+hipError_t launch_make_fixed_records(uint64_t* off, uint32_t* len, uint64_t count, uint64_t stride,
+                                     uint32_t length, hipStream_t stream);
+
+hipError_t launch_fill_splitmix(void* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
+                                hipStream_t stream);
+
+}  // namespace mi_crc

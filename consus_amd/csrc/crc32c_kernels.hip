@@ -1,0 +1,715 @@
+// consus_amd/csrc/crc32c_kernels.hip -- CDNA4 (gfx950) CRC-32C kernels.
+//
+// Re-implements the per-record checksum of consus::crc32c
+// (common/crc32c.h:40-41, common/crc32c.cc:122-126) for batches of
+// independent durable-log records (txman/durable_log.cc:215-218).
+// Bit-exact with the reference; parity tests in tests/test_gpu_parity.py.
+//
+// Work decomposition:
+//   * a "team" of 8 lanes owns one record (or one 4 KiB chunk of one);
+//     a row is 128 contiguous bytes, 16 B per lane (global_load_dwordx4),
+//     so each wave-wide load moves 8 full 128-B lines;
+//   * each lane keeps 4 independent raw-CRC chains V_q, one per dword of its
+//     16-B column, with stride 32 dwords: V <- Z_128(V) ^ d.  Z_128 is applied
+//     with 4 lookups into "fold" tables staged in LDS in a bank-private layout
+//     (each of the 32 lanes of a ds_read_b32 group owns its own bank, so the
+//     lookups are conflict-free whatever the data), addressed by ONE v_perm_b32
+//     per lookup;
+//   * at the end of a record the 32 chains of a team are folded with the
+//     slice-by-16 tables and a 3-level lane tree (Z_16, Z_32, Z_64).
+// No MFMA: this is a GF(2) scan; the bound is HBM read bandwidth.
+#include <hip/hip_runtime.h>
+
+#include "crc32c_kernels.h"
+
+namespace mi_crc {
+
+extern __shared__ __attribute__((aligned(16))) char smem[];
+
+// The record kernels declare no static LDS, so the dynamic image starts at
+// LDS address 0 (checked by tests/test_build.py on the ISA metadata) and a
+// table byte offset IS the ds_read address: no base add per lookup.
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t lds32(uint32_t byte_addr)
+{
+    return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(byte_addr));
+}
+
+// Stage the table image into LDS: G^{128} replicated 32x bank-private, then
+// T_0..T_15, G^{32}, G^{64} verbatim.  Byte address of G^{128}_t[b] for the
+// lane whose ds_read_b32 group position is c (= lane & 31):
+//   (t >> 1) * 65536 + b * 256 + (t & 1) * 128 + c * 4   ->  bank == c.
+__device__ __forceinline__ void stage_tables(const uint32_t* __restrict__ g)
+{
+    for (uint32_t i = threadIdx.x; i < 1024u * 8u; i += blockDim.x)
+    {
+        const uint32_t e = i >> 3;          // t * 256 + b
+        const uint32_t c4 = (i & 7u) * 4u;  // first of 4 consecutive copies
+        const uint32_t t = e >> 8, b = e & 255u;
+        const uint32_t v = g[kTabMain + e];
+        const uint32_t addr = (t >> 1) * 65536u + b * 256u + (t & 1u) * 128u + c4 * 4u;
+        *reinterpret_cast<uint4*>(smem + kLdsMain + addr) = make_uint4(v, v, v, v);
+    }
+    const uint4* src = reinterpret_cast<const uint4*>(g + kTabT);
+    uint4* dst = reinterpret_cast<uint4*>(smem + kLdsT);
+    for (uint32_t i = threadIdx.x; i < (4096u + 2048u) / 4u; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+// Lane info for the v_perm address builder: byte0 = c*4, byte1 = c*4 + 128,
+// byte2 = 0, byte3 = 1 (the 64 KiB half for tables 2 and 3).
+__device__ __forceinline__ uint32_t lane_info()
+{
+    const uint32_t c4 = (threadIdx.x & 31u) * 4u;
+    return c4 | ((c4 + 128u) << 8) | (1u << 24);
+}
+
+// Z_128 lookups (row_update): v_perm_b32 builds {lane byte, v.byte_t, half
+// bit, 0} = the LDS byte address of G^{128}_t[v.byte_t] in this lane's
+// private bank.  Selector bytes 0-3 pick v (src1), 4-7 pick li (src0),
+// 0x0C gives 0x00.
+
+// Z_{4m}(v) from the slice-by-16 tables: byte j uses T_{4m-1-j}.
+template <int M>
+__device__ __forceinline__ uint32_t zT(uint32_t v)
+{
+    constexpr uint32_t k0 = kLdsT + (4 * M - 1) * 1024;
+    return lds32(k0 + ((v & 0xFFu) << 2)) ^ lds32(k0 - 1024 + ((v >> 6) & 0x3FCu)) ^
+           lds32(k0 - 2048 + ((v >> 14) & 0x3FCu)) ^ lds32(k0 - 3072 + ((v >> 22) & 0x3FCu));
+}
+
+// Z_n(v) from a G^n table set at LDS byte offset `base` (byte j uses G_j).
+__device__ __forceinline__ uint32_t zG(uint32_t base, uint32_t v)
+{
+    return lds32(base + ((v & 0xFFu) << 2)) ^ lds32(base + 1024 + ((v >> 6) & 0x3FCu)) ^
+           lds32(base + 2048 + ((v >> 14) & 0x3FCu)) ^ lds32(base + 3072 + ((v >> 22) & 0x3FCu));
+}
+
+// One 128-B row: each lane folds its 16 bytes into its four chains.
+// All 16 addresses, then all 16 lookups, then the XORs, so a wave keeps 16
+// conflict-free ds_read_b32 in flight per row.
+__device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint32_t li)
+{
+    uint32_t a[16], r[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        a[4 * q + 0] = __builtin_amdgcn_perm(li, V[q], 0x0C060004u);
+        a[4 * q + 1] = __builtin_amdgcn_perm(li, V[q], 0x0C060105u);
+        a[4 * q + 2] = __builtin_amdgcn_perm(li, V[q], 0x0C070204u);
+        a[4 * q + 3] = __builtin_amdgcn_perm(li, V[q], 0x0C070305u);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = lds32(kLdsMain + a[i]);
+    V[0] = r[0] ^ r[1] ^ r[2] ^ r[3] ^ d.x;
+    V[1] = r[4] ^ r[5] ^ r[6] ^ r[7] ^ d.y;
+    V[2] = r[8] ^ r[9] ^ r[10] ^ r[11] ^ d.z;
+    V[3] = r[12] ^ r[13] ^ r[14] ^ r[15] ^ d.w;
+}
+
+// Fold a team's 32 chains into the raw CRC of the team's bytes, assuming the
+// last processed row ends exactly at the end of those bytes.  Valid in lane
+// (lane & 7) == 0 of the team.  DESIGN.md section 3.2:
+//   raw = XOR_L Z_{16(7-L)}( Z16 V0 ^ Z12 V1 ^ Z8 V2 ^ Z4 V3 )_L
+__device__ __forceinline__ uint32_t team_fold(const uint32_t (&V)[4])
+{
+    const uint32_t x = zT<4>(V[0]) ^ zT<3>(V[1]) ^ zT<2>(V[2]) ^ zT<1>(V[3]);
+    const uint32_t y = zT<4>(x) ^ __shfl_xor(x, 1);
+    const uint32_t w = zG(kLdsZ32, y) ^ __shfl_xor(y, 2);
+    return zG(kLdsZ64, w) ^ __shfl_xor(w, 4);
+}
+
+__device__ __forceinline__ uint4 load16(const uint8_t* p)
+{
+    return *reinterpret_cast<const uint4*>(p);
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-stride batches: record i = [base + i*stride, +len), base and stride
+// 16-byte aligned, len a multiple of 16 (other shapes take the variable path).
+// Persistent grid (one 1024-thread workgroup per CU, 152 KiB LDS); team t
+// handles records t, t + nteams, ...  Each step issues two groups (16 KiB
+// per wave, 16 dwordx4 per lane) and consumes them in the same step, so the
+// compiler's vmcnt accounting stays exact (no loop-carried loads, which it
+// would drain with vmcnt(0)); 16 waves per CU keep >= 128 KiB in flight.
+// ---------------------------------------------------------------------------
+template <bool PADDED, bool INITS>
+__global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_kernel(
+    const uint8_t* __restrict__ base, uint64_t stride, uint32_t len, uint32_t groups,
+    const uint32_t* __restrict__ inits, uint64_t init_stride, uint64_t count,
+    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables)
+{
+    stage_tables(tables);
+
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t li = lane_info();
+    const uint64_t team = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kTeam;
+    const uint64_t nteams = uint64_t(gridDim.x) * kBlock / kTeam;
+    const uint64_t team0 = team & ~uint64_t(7);  // first team of this wave
+    const uint64_t iters = team0 < count ? (count - team0 + nteams - 1) / nteams : 0;
+
+    // Byte offset (from the record start) of this lane's column in row 0 of
+    // group 0; negative in the leading pad when len is not a multiple of 1 KiB.
+    const int32_t pad = int32_t(groups * kGroupBytes) - int32_t(len);
+    const int32_t col0 = int32_t(tl) * 16 - pad;
+    // Row/lane holding the record's first dword (where ~init is folded in).
+    const uint32_t r0 = uint32_t(pad) / kRowBytes;
+    const bool init_lane = tl == (uint32_t(pad) % kRowBytes) / 16u;
+
+    for (uint64_t it = 0; it < iters; ++it)
+    {
+        // Teams past the end re-hash the last record (loads stay
+        // unconditional) and do not store.
+        const uint64_t rec_raw = team + it * nteams;
+        const uint64_t rec = rec_raw < count ? rec_raw : count - 1;
+        const uint8_t* rbase = base + rec * stride;
+        uint32_t init_word = INITS ? inits[rec * init_stride] : 0u;  // inverted at use
+        uint32_t V[4] = {0, 0, 0, 0};
+        for (uint32_t g = 0; g < groups; g += 2)
+        {
+            // Both groups are always loaded (a lone group re-reads itself) so
+            // the compiler counts 16 outstanding loads at the first use.
+            const bool two = g + 1 < groups;
+            const uint32_t gb = two ? g + 1 : g;
+            uint4 A[kGroupRows], B[kGroupRows];
+#pragma unroll
+            for (int r = 0; r < kGroupRows; ++r)
+            {
+                const int32_t o = col0 + int32_t(g) * kGroupBytes + r * kRowBytes;
+                A[r] = load16(PADDED && o < 0 ? rbase : rbase + o);
+            }
+#pragma unroll
+            for (int r = 0; r < kGroupRows; ++r)
+            {
+                const int32_t o = col0 + int32_t(gb) * kGroupBytes + r * kRowBytes;
+                B[r] = load16(PADDED && o < 0 ? rbase : rbase + o);
+            }
+            // keep the init word's wait behind the data loads (no hoisting)
+            if (INITS) asm volatile("" : "+v"(init_word));
+            if (PADDED)
+            {
+#pragma unroll
+                for (int r = 0; r < kGroupRows; ++r)
+                {
+                    const int32_t o = col0 + int32_t(g) * kGroupBytes + r * kRowBytes;
+                    if (o < 0) A[r] = make_uint4(0, 0, 0, 0);
+                }
+            }
+            const uint32_t x = (g == 0 && init_lane) ? ~init_word : 0u;  // ~0 = 0xFFFFFFFF for init 0
+            if (PADDED)
+            {
+#pragma unroll
+                for (int r = 0; r < kGroupRows; ++r)
+                    if (uint32_t(r) == r0) A[r].x ^= x;
+            }
+            else
+                A[0].x ^= x;
+#pragma unroll
+            for (int r = 0; r < kGroupRows; ++r) row_update(V, A[r], li);
+            if (two)
+            {
+#pragma unroll
+                for (int r = 0; r < kGroupRows; ++r) row_update(V, B[r], li);
+            }
+        }
+        const uint32_t raw = team_fold(V);
+        if (tl == 0 && rec_raw < count) out[rec] = ~raw;
+    }
+}
+
+hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const uint32_t* inits,
+                        uint64_t count, uint32_t* out, const uint32_t* tables, int grid,
+                        hipStream_t stream)
+{
+    const uint32_t* zero_word = tables + kTabZero;
+    if (count == 0) return hipSuccess;
+    const uint32_t groups = (len + kGroupBytes - 1) / kGroupBytes;
+    const uint64_t need = (count + (kBlock / kTeam) - 1) / (kBlock / kTeam);
+    if (uint64_t(grid) > need) grid = int(need);
+    const bool padded = len != groups * kGroupBytes;
+    const uint32_t* ip = inits ? inits : zero_word;
+    const uint64_t is = inits ? 1 : 0;
+    const uint8_t* b = static_cast<const uint8_t*>(base);
+#define MI_LAUNCH_FIXED(P, I)                                                                   \
+    hipLaunchKernelGGL((crc32c_fixed_kernel<P, I>), dim3(grid), dim3(kBlock), kLdsBytes, stream, \
+                       b, stride, len, groups, ip, is, count, out, tables)
+    if (padded && inits)
+        MI_LAUNCH_FIXED(true, true);
+    else if (padded)
+        MI_LAUNCH_FIXED(true, false);
+    else if (inits)
+        MI_LAUNCH_FIXED(false, true);
+    else
+        MI_LAUNCH_FIXED(false, false);
+#undef MI_LAUNCH_FIXED
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Variable-length batches: plan -> chunks -> finalize.
+//   plan:     each record's 16-aligned main part [a, e) is cut into 4 KiB
+//             chunks aligned backward from e plus one head chunk of the
+//             remainder; chunks are bucketed by their 1-KiB group count
+//             (4 first) so the 8 teams of a wave get equal work.
+//   chunks:   one team per chunk -> raw CRC of the chunk (partial[item]).
+//   finalize: one thread per record: Horner over its chunks with Z_4096,
+//             then the <16-byte tail byte-serially; short records entirely
+//             byte-serially.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPlanBlock = 256;
+
+uint32_t var_plan_blocks(uint64_t count)
+{
+    return uint32_t((count + kPlanBlock - 1) / kPlanBlock);
+}
+
+struct RecShape
+{
+    uint64_t e;      // 16-aligned end of the main part
+    uint32_t nfull;  // full 4 KiB chunks
+    uint32_t rem;    // bytes in the head chunk (0 = none)
+    uint32_t hbin;   // 1..4 groups of the head chunk, 0 = none
+};
+
+__device__ __forceinline__ RecShape rec_shape(uint64_t a, uint32_t L)
+{
+    RecShape s{0, 0, 0, 0};
+    if (L < uint32_t(kSmallRecord)) return s;
+    s.e = (a + L) & ~uint64_t(15);
+    const uint64_t m = s.e - a;
+    s.nfull = uint32_t(m / kChunk);
+    s.rem = uint32_t(m % kChunk);
+    s.hbin = s.rem ? (s.rem + kGroupBytes - 1) / kGroupBytes : 0;
+    return s;
+}
+
+// Block-wide exclusive scan of one u32 per thread (256 threads, 4 waves).
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t& total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= uint32_t(d)) x += y;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    uint32_t woff = 0;
+    total = 0;
+    for (uint32_t w = 0; w < kPlanBlock / 64; ++w)
+    {
+        if (w < wave) woff += sh[w];
+        total += sh[w];
+    }
+    __syncthreads();
+    return woff + x - v;
+}
+
+__global__ __launch_bounds__(kPlanBlock) void plan_count_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, uint64_t count, uint32_t* __restrict__ blk, uint32_t nblocks)
+{
+    __shared__ uint32_t sh[kPlanBlock / 64];
+    const uint64_t r = uint64_t(blockIdx.x) * kPlanBlock + threadIdx.x;
+    RecShape s{0, 0, 0, 0};
+    if (r < count) s = rec_shape(uint64_t(base) + off[r], len[r]);
+    uint32_t c[4];
+    c[0] = s.nfull + (s.hbin == 4);  // bin order: 4, 3, 2, 1 groups
+    c[1] = s.hbin == 3;
+    c[2] = s.hbin == 2;
+    c[3] = s.hbin == 1;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+    {
+        uint32_t total;
+        block_exscan(c[b], sh, total);
+        if (threadIdx.x == 0) blk[b * nblocks + blockIdx.x] = total;
+    }
+}
+
+// Single-workgroup exclusive scan over n u32 (in place); writes the grand
+// total to blk[n].  n = 4 * nblocks is small (16K for 1M records).
+__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ blk, uint32_t n)
+{
+    __shared__ uint32_t sh[16];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t base = 0; base < n; base += 1024)
+    {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < n ? blk[i] : 0;
+        uint32_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane >= uint32_t(d)) x += y;
+        }
+        if (lane == 63) sh[wave] = x;
+        __syncthreads();
+        uint32_t woff = 0, tot = 0;
+        for (uint32_t w = 0; w < 16; ++w)
+        {
+            if (w < wave) woff += sh[w];
+            tot += sh[w];
+        }
+        const uint32_t c = carry;
+        if (i < n) blk[i] = c + woff + x - v;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = c + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) blk[n] = carry;
+}
+
+__global__ __launch_bounds__(kPlanBlock) void plan_scatter_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, uint64_t count, const uint32_t* __restrict__ blk,
+    uint32_t nblocks, Item* __restrict__ items, uint64_t item_cap,
+    uint32_t* __restrict__ full_pos, uint32_t* __restrict__ head_pos)
+{
+    __shared__ uint32_t sh[kPlanBlock / 64];
+    const uint64_t r = uint64_t(blockIdx.x) * kPlanBlock + threadIdx.x;
+    RecShape s{0, 0, 0, 0};
+    if (r < count) s = rec_shape(uint64_t(base) + off[r], len[r]);
+    uint32_t c[4] = {s.nfull + (s.hbin == 4), s.hbin == 3, s.hbin == 2, s.hbin == 1};
+    uint32_t pos[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+    {
+        uint32_t total;
+        pos[b] = blk[b * nblocks + blockIdx.x] + block_exscan(c[b], sh, total);
+    }
+    if (r >= count) return;
+    const uint32_t total_items = blk[4 * nblocks];
+    if (total_items > item_cap) return;  // host re-plans with a larger workspace
+    const uint32_t rid = uint32_t(r);
+    for (uint32_t j = 0; j < s.nfull; ++j)
+    {
+        // The earliest full chunk also carries init bytes when the head
+        // chunk holds fewer than 4 bytes (or there is none): record start =
+        // chunk start - rem.
+        Item it;
+        it.end = s.e - uint64_t(j) * kChunk;
+        const bool first = j + 1 == s.nfull && s.rem < 4;
+        it.len = kChunk | (first ? s.rem << kItemShiftBit : 0u);
+        it.rec_flag = rid | (first ? kItemStart : 0u);
+        items[pos[0] + j] = it;
+    }
+    full_pos[r] = pos[0];
+    if (s.hbin)
+    {
+        const uint32_t hp = s.hbin == 4 ? pos[0] + s.nfull : pos[4 - s.hbin];
+        Item it;
+        it.end = s.e - uint64_t(s.nfull) * kChunk;
+        it.len = s.rem;
+        it.rec_flag = rid | kItemStart;
+        items[hp] = it;
+        head_pos[r] = hp;
+    }
+}
+
+hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                           uint64_t count, const VarWorkspace& ws, hipStream_t stream)
+{
+    const uint32_t nb = var_plan_blocks(count);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(nb), dim3(kPlanBlock), 0, stream,
+                       static_cast<const uint8_t*>(base), offsets, lengths, count, ws.blk, nb);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, 4 * nb);
+    hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanBlock), 0, stream,
+                       static_cast<const uint8_t*>(base), offsets, lengths, count, ws.blk, nb,
+                       ws.items, ws.item_cap, ws.full_pos, ws.head_pos);
+    return hipGetLastError();
+}
+
+// Fold ~init into the record's first 4 bytes, then zero every byte below the
+// chunk start.  `o` = byte offset of this lane's 16 B from the chunk start,
+// `shift` = chunk start - record start (0..3).
+__device__ __forceinline__ uint4 head_fix(uint4 d, int32_t o, bool start, uint32_t xinit,
+                                          int32_t shift)
+{
+    uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        const int32_t rel = o + shift + 4 * q;  // from the record start
+        if (start && rel > -4 && rel < 4)
+            w[q] ^= rel >= 0 ? (xinit >> (8 * rel)) : (xinit << (8 * -rel));
+        const int32_t oc = o + 4 * q;  // from the chunk start
+        if (oc <= -4)
+            w[q] = 0;
+        else if (oc < 0)
+            w[q] &= 0xFFFFFFFFu << (8 * -oc);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
+    const Item* __restrict__ items, const uint32_t* __restrict__ total_items,
+    const uint32_t* __restrict__ inits, uint32_t* __restrict__ partial, uint64_t item_cap,
+    const uint32_t* __restrict__ tables)
+{
+    stage_tables(tables);
+    const uint32_t n_items = *total_items;
+    if (n_items > item_cap) return;
+
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t li = lane_info();
+    const uint32_t team = (blockIdx.x * kBlock + threadIdx.x) / kTeam;
+    const uint32_t nteams = gridDim.x * kBlock / kTeam;
+    const uint32_t team0 = team & ~7u;
+
+    for (uint32_t w0 = team0; w0 < n_items; w0 += nteams)
+    {
+        const uint32_t idx = w0 + (team - team0);
+        const bool valid = idx < n_items;
+        Item it{16, 0, 0};
+        if (valid) it = items[idx];
+        const int32_t shift = int32_t(it.len >> kItemShiftBit);
+        it.len &= kItemLenMask;
+        const uint32_t gt = (it.len + kGroupBytes - 1) / kGroupBytes;
+        // wave-uniform group count = max over the 8 teams
+        uint32_t gw = gt;
+        gw = max(gw, uint32_t(__shfl_xor(int(gw), 8)));
+        gw = max(gw, uint32_t(__shfl_xor(int(gw), 16)));
+        gw = max(gw, uint32_t(__shfl_xor(int(gw), 32)));
+        const bool start = (it.rec_flag & kItemStart) != 0;
+        const uint32_t xinit =
+            start ? (inits ? ~inits[it.rec_flag & ~kItemStart] : 0xFFFFFFFFu) : 0u;
+        // offset of this lane's column in row 0 of group 0, relative to chunk start
+        const int32_t o0 = int32_t(it.len) - int32_t(gw * kGroupBytes) + int32_t(tl) * 16;
+        const uint8_t* p0 = reinterpret_cast<const uint8_t*>(it.end) - int64_t(gw) * kGroupBytes +
+                            int64_t(tl) * 16;
+
+        uint32_t V[4] = {0, 0, 0, 0};
+        uint4 A[kGroupRows], B[kGroupRows];
+        auto issue = [&](uint4 (&buf)[kGroupRows], uint32_t g) {
+#pragma unroll
+            for (int r = 0; r < kGroupRows; ++r)
+            {
+                const int32_t o = o0 + int32_t(g) * kGroupBytes + r * kRowBytes;
+                buf[r] = (valid && o > -16)
+                             ? load16(p0 + int64_t(g) * kGroupBytes + r * kRowBytes)
+                             : make_uint4(0, 0, 0, 0);
+            }
+        };
+        auto process = [&](uint4 (&buf)[kGroupRows], uint32_t g) {
+#pragma unroll
+            for (int r = 0; r < kGroupRows; ++r)
+            {
+                const int32_t o = o0 + int32_t(g) * kGroupBytes + r * kRowBytes;
+                uint4 d = buf[r];
+                if (__builtin_expect(o > -20 && o < 4, 0)) d = head_fix(d, o, start, xinit, shift);
+                row_update(V, d, li);
+            }
+        };
+        issue(A, 0);
+        if (gw > 1) issue(B, 1);
+        for (uint32_t g = 0; g < gw; g += 2)
+        {
+            process(A, g);
+            if (g + 2 < gw) issue(A, g + 2);
+            if (g + 1 < gw)
+            {
+                process(B, g + 1);
+                if (g + 3 < gw) issue(B, g + 3);
+            }
+        }
+        const uint32_t raw = team_fold(V);
+        if (valid && tl == 0) partial[idx] = raw;
+    }
+}
+
+hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
+                             const uint32_t* tables, int grid, hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    const uint32_t* total = ws.blk + 4 * var_plan_blocks(count);
+    hipLaunchKernelGGL(crc32c_chunk_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream, ws.items,
+                       total, inits, ws.partial, ws.item_cap, tables);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void crc32c_finalize_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
+    const uint32_t* __restrict__ partial, const uint32_t* __restrict__ full_pos,
+    const uint32_t* __restrict__ head_pos, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables)
+{
+    __shared__ uint32_t t0[256];
+    __shared__ uint32_t zc[1024];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) t0[i] = tables[kTabT + i];
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) zc[i] = tables[kTabZChunk + i];
+    __syncthreads();
+    const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= count) return;
+    const uint8_t* p = base + off[r];
+    const uint32_t L = len[r];
+    const uint32_t init = inits ? inits[r] : 0u;
+    const RecShape s = rec_shape(uint64_t(p), L);
+    uint32_t c;
+    uint64_t tail_from;
+    if (L < uint32_t(kSmallRecord))
+    {
+        c = ~init;
+        tail_from = 0;
+    }
+    else
+    {
+        c = s.hbin ? partial[head_pos[r]] : 0u;
+        const uint32_t fp = full_pos[r];
+        for (uint32_t j = s.nfull; j-- > 0;)
+            c = (zc[c & 0xFFu] ^ zc[256 + ((c >> 8) & 0xFFu)] ^ zc[512 + ((c >> 16) & 0xFFu)] ^
+                 zc[768 + (c >> 24)]) ^
+                partial[fp + j];
+        tail_from = s.e - uint64_t(p);
+    }
+    for (uint64_t i = tail_from; i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+    out[r] = ~c;
+}
+
+hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                               const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
+                               uint32_t* out, const uint32_t* tables, hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    const uint32_t nb = uint32_t((count + 255) / 256);
+    hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(nb), dim3(256), 0, stream,
+                       static_cast<const uint8_t*>(base), offsets, lengths, inits, count,
+                       ws.partial, ws.full_pos, ws.head_pos, out, tables);
+    return hipGetLastError();
+}
+
+// Offsets/lengths for a fixed-stride batch the fast kernel cannot take
+// (unaligned base/stride or a length that is not a multiple of 16).
+__global__ __launch_bounds__(256) void make_fixed_records_kernel(uint64_t* __restrict__ off,
+                                                                 uint32_t* __restrict__ len,
+                                                                 uint64_t count, uint64_t stride,
+                                                                 uint32_t length)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    off[i] = i * stride;
+    len[i] = length;
+}
+
+hipError_t launch_make_fixed_records(uint64_t* off, uint32_t* len, uint64_t count, uint64_t stride,
+                                     uint32_t length, hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(make_fixed_records_kernel, dim3(uint32_t((count + 255) / 256)), dim3(256),
+                       0, stream, off, len, count, stride, length);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// combine: out[i] = Z_{len_b[i]}(crc_a[i]) ^ crc_b[i]  (crc32c(0, A||B) from
+// crc32c(0, A), crc32c(0, B) and |B|).  pow2_tables holds G^{2^k}, k = 0..47.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void crc32c_combine_kernel(
+    const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+    const uint64_t* __restrict__ nb, uint64_t count, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ pow2)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    uint32_t s = a[i];
+    uint64_t n = nb[i];
+    for (int k = 0; n && k < 48; ++k, n >>= 1)
+    {
+        if (n & 1u)
+        {
+            const uint32_t* g = pow2 + k * 1024;
+            s = g[s & 0xFFu] ^ g[256 + ((s >> 8) & 0xFFu)] ^ g[512 + ((s >> 16) & 0xFFu)] ^
+                g[768 + (s >> 24)];
+        }
+    }
+    out[i] = s ^ b[i];
+}
+
+hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,
+                          uint64_t count, uint32_t* out, const uint32_t* pow2_tables,
+                          hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(crc32c_combine_kernel, dim3(uint32_t((count + 255) / 256)), dim3(256), 0,
+                       stream, crc_a, crc_b, len_b, count, out, pow2_tables);
+    return hipGetLastError();
+}
+
+// Allow the 152 KiB dynamic LDS image on the two persistent kernels.
+hipError_t configure_kernels()
+{
+    const void* k[] = {reinterpret_cast<const void*>(&crc32c_fixed_kernel<false, false>),
+                       reinterpret_cast<const void*>(&crc32c_fixed_kernel<false, true>),
+                       reinterpret_cast<const void*>(&crc32c_fixed_kernel<true, false>),
+                       reinterpret_cast<const void*>(&crc32c_fixed_kernel<true, true>)};
+    hipError_t e = hipSuccess;
+    for (const void* f : k)
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_chunk_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    return e;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic input: u64 word j of the stream = splitmix64(seed ^ j).
+// dst must be 8-byte aligned and byte_offset a multiple of 8.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* __restrict__ dst,
+                                                            uint64_t nbytes, uint64_t seed,
+                                                            uint64_t word0)
+{
+    const uint64_t nwords = nbytes / 8;
+    const uint64_t npairs = nwords / 2;
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+    for (; i < npairs; i += step)
+    {
+        ulonglong2 v;
+        v.x = splitmix64(seed ^ (word0 + 2 * i));
+        v.y = splitmix64(seed ^ (word0 + 2 * i + 1));
+        reinterpret_cast<ulonglong2*>(dst)[i] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+    {
+        for (uint64_t w = npairs * 2; w < nwords; ++w)
+            reinterpret_cast<uint64_t*>(dst)[w] = splitmix64(seed ^ (word0 + w));
+        const uint64_t tail = nbytes & 7u;
+        if (tail)
+        {
+            const uint64_t v = splitmix64(seed ^ (word0 + nwords));
+            for (uint64_t k = 0; k < tail; ++k) dst[nwords * 8 + k] = uint8_t(v >> (8 * k));
+        }
+    }
+}
+
+hipError_t launch_fill_splitmix(void* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
+                                hipStream_t stream)
+{
+    if (nbytes == 0) return hipSuccess;
+    const uint64_t pairs = nbytes / 16 + 1;
+    uint64_t grid = (pairs + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(fill_splitmix_kernel, dim3(uint32_t(grid)), dim3(256), 0, stream,
+                       static_cast<uint8_t*>(dst), nbytes, seed, byte_offset / 8);
+    return hipGetLastError();
+}
+
+}  // namespace mi_crc

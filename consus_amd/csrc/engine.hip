@@ -1,0 +1,807 @@
+// consus_amd/csrc/engine.hip -- host side of the MI355X CRC-32C engine:
+// the C ABI of include/consus_crc32c.h.
+//
+// Owns: device selection and the operator-table image (uploaded once),
+// one HIP stream + grow-only workspaces per calling thread (the reference
+// function is called concurrently by N txman worker threads,
+// txman/durable_log.cc:215-218 runs outside m_mtx), staging of host batches,
+// the streaming pipeline, and the RCCL communicator.
+//
+// No CRC over payload bytes is ever computed on the host here: every checksum
+// comes from the kernels in crc32c_kernels.hip.  Host code only does
+// operator algebra (table construction, combine of finished CRCs).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/consus_crc32c.h"
+#include "crc32c_kernels.h"
+#include "crc32c_math.h"
+
+using namespace mi_crc;
+
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int status, const std::string& msg)
+{
+    t_err = msg;
+    return status;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(MI_CRC32C_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DeviceState
+{
+    int ordinal = -1;
+    int cus = 0;
+    uint32_t* d_tables = nullptr;  // kTabWords
+    uint32_t* d_pow2 = nullptr;    // 48 x 1024: G^{2^k}
+    Op32 pow2_ops[64];             // host copies for mi_crc32c_combine
+    std::string arch;
+};
+
+std::mutex g_mu;
+std::atomic<DeviceState*> g_dev{nullptr};
+
+int init_device(int device)
+{
+    std::lock_guard<std::mutex> lock(g_mu);
+    if (DeviceState* d = g_dev.load())
+    {
+        if (d->ordinal == device || device < 0) return MI_CRC32C_OK;
+        return fail(MI_CRC32C_EINVAL, "engine already initialised on another device");
+    }
+    if (device < 0) device = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device)
+        return fail(MI_CRC32C_ENODEV, "no HIP device " + std::to_string(device));
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    std::string arch = prop.gcnArchName;
+    if (arch.find("gfx950") == std::string::npos)
+        return fail(MI_CRC32C_ENODEV, "device " + std::to_string(device) + " is " + arch +
+                                          "; this engine is built for gfx950 (MI355X) only");
+    auto* d = new DeviceState;
+    d->ordinal = device;
+    d->cus = prop.multiProcessorCount;
+    d->arch = arch;
+
+    // Operator-table image (crc32c_math.h): G^{128}, T_0..T_15, G^{32}, G^{64}, G^{4096}.
+    std::vector<uint32_t> img(kTabWords);
+    make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabMain]), kRowBytes);
+    make_slice16_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabT]));
+    make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZ32]), 32);
+    make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZ64]), 64);
+    make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZChunk]), kChunk);
+    std::vector<uint32_t> pow2(48 * 1024);
+    Op32 p = Op32::zero_byte();
+    for (int k = 0; k < 64; ++k)
+    {
+        d->pow2_ops[k] = p;
+        if (k < 48)
+            for (int j = 0; j < 4; ++j)
+                for (uint32_t b = 0; b < 256; ++b) pow2[k * 1024 + j * 256 + b] = p.apply(b << (8 * j));
+        p = p.then(p);
+    }
+    hipError_t e = hipMalloc(&d->d_tables, img.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&d->d_pow2, pow2.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(d->d_tables, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d->d_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = configure_kernels();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess)
+    {
+        delete d;
+        return fail(MI_CRC32C_EHIP, std::string("table upload: ") + hipGetErrorString(e));
+    }
+    g_dev.store(d);
+    return MI_CRC32C_OK;
+}
+
+DeviceState* dev_or_init(int* status)
+{
+    DeviceState* d = g_dev.load();
+    if (d) return d;
+    *status = init_device(0);
+    return g_dev.load();
+}
+
+// Grow-only device buffer.
+struct DevBuf
+{
+    void* p = nullptr;
+    size_t cap = 0;
+    int reserve(size_t bytes)
+    {
+        if (bytes <= cap) return MI_CRC32C_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        want = want + want / 4;
+        if (hipMalloc(&p, want) != hipSuccess)
+            return fail(MI_CRC32C_ENOMEM, "hipMalloc(" + std::to_string(want) + ") failed");
+        cap = want;
+        return MI_CRC32C_OK;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct PinBuf
+{
+    void* p = nullptr;
+    size_t cap = 0;
+    int reserve(size_t bytes)
+    {
+        if (bytes <= cap) return MI_CRC32C_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess)
+            return fail(MI_CRC32C_ENOMEM, "hipHostMalloc(" + std::to_string(want) + ") failed");
+        cap = want;
+        return MI_CRC32C_OK;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+// Per-(thread or pipeline slot) execution context.
+struct Ctx
+{
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+    DevBuf data, off, len, inits, out;  // staging of host batches
+    DevBuf items, partial, full_pos, head_pos, blk;
+    PinBuf pin_small;                   // plan-size read-back, small host outputs
+
+    int open(int ordinal)
+    {
+        HIP_TRY(hipSetDevice(ordinal));
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreate(&ev0));
+        HIP_TRY(hipEventCreate(&ev1));
+        HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        return pin_small.reserve(4096);
+    }
+};
+
+thread_local Ctx* t_ctx = nullptr;
+
+Ctx* thread_ctx(int* status)
+{
+    DeviceState* d = dev_or_init(status);
+    if (!d) return nullptr;
+    if (t_ctx) return t_ctx;
+    auto* c = new Ctx;  // per-thread, never freed (threads are few and long-lived)
+    *status = c->open(d->ordinal);
+    if (*status != MI_CRC32C_OK)
+    {
+        delete c;
+        return nullptr;
+    }
+    t_ctx = c;
+    return c;
+}
+
+uint32_t apply_zeros(const DeviceState* d, uint32_t s, uint64_t n)
+{
+    for (int k = 0; n && k < 64; ++k, n >>= 1)
+        if (n & 1u) s = d->pow2_ops[k].apply(s);
+    return s;
+}
+
+// ---- the variable-length pipeline on device-resident arrays -------------
+// All pointers device pointers; enqueued on c->stream.  `total_bytes` bounds
+// the plan size (0 = unknown -> one read-back).
+int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
+            const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
+{
+    if (count == 0) return MI_CRC32C_OK;
+    if (count >= (1ull << 31)) return fail(MI_CRC32C_EINVAL, "count >= 2^31 records");
+    const uint32_t nb = var_plan_blocks(count);
+    int st;
+    if ((st = c->blk.reserve((4 * size_t(nb) + 4) * 4)) ||
+        (st = c->full_pos.reserve(count * 4)) || (st = c->head_pos.reserve(count * 4)))
+        return st;
+    uint64_t cap = total_bytes ? total_bytes / kChunk + 2 * uint64_t(count) + 1
+                               : std::max<uint64_t>(c->items.cap / sizeof(Item), 2 * count + 1);
+    for (int attempt = 0; attempt < 2; ++attempt)
+    {
+        if (cap >= (1ull << 32)) return fail(MI_CRC32C_EINVAL, "plan exceeds 2^32 chunks");
+        if ((st = c->items.reserve(cap * sizeof(Item))) || (st = c->partial.reserve(cap * 4)))
+            return st;
+        cap = std::min<uint64_t>(c->items.cap / sizeof(Item), c->partial.cap / 4);
+        VarWorkspace ws{c->blk.as<uint32_t>(), c->items.as<Item>(), c->partial.as<uint32_t>(),
+                        c->full_pos.as<uint32_t>(), c->head_pos.as<uint32_t>(), cap};
+        HIP_TRY(launch_var_plan(base, off, len, count, ws, c->stream));
+        if (!total_bytes)
+        {
+            uint32_t* h = c->pin_small.as<uint32_t>();
+            HIP_TRY(hipMemcpyAsync(h, c->blk.as<uint32_t>() + 4 * nb, 4, hipMemcpyDeviceToHost,
+                                   c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (*h > cap)
+            {
+                cap = *h;
+                continue;
+            }
+        }
+        const uint64_t want_grid = (cap + (kBlock / kTeam) - 1) / (kBlock / kTeam);
+        const int grid = int(std::min<uint64_t>(uint64_t(d->cus), std::max<uint64_t>(want_grid, 1)));
+        HIP_TRY(launch_var_chunks(inits, count, ws, d->d_tables, grid, c->stream));
+        HIP_TRY(launch_var_finalize(base, off, len, inits, count, ws, out, d->d_tables, c->stream));
+        return MI_CRC32C_OK;
+    }
+    return fail(MI_CRC32C_EHIP, "plan size did not converge");
+}
+
+bool fixed_fast_ok(const void* base, uint64_t stride, uint64_t length)
+{
+    return (uintptr_t(base) % 16) == 0 && (stride % 16) == 0 && (length % 16) == 0 &&
+           length >= 16 && length <= (1ull << 30) && stride >= length;
+}
+
+int run_fixed(DeviceState* d, Ctx* c, const void* base, uint64_t stride, uint64_t length,
+              const uint32_t* inits, size_t count, uint32_t* out)
+{
+    if (count == 0) return MI_CRC32C_OK;
+    if (fixed_fast_ok(base, stride, length))
+    {
+        HIP_TRY(launch_fixed(base, stride, uint32_t(length), inits, count, out, d->d_tables,
+                             d->cus, c->stream));
+        return MI_CRC32C_OK;
+    }
+    if (length > 0xFFFFFFFFull) return fail(MI_CRC32C_EINVAL, "fixed length >= 4 GiB");
+    int st;
+    if ((st = c->off.reserve(count * 8)) || (st = c->len.reserve(count * 4))) return st;
+    HIP_TRY(launch_make_fixed_records(c->off.as<uint64_t>(), c->len.as<uint32_t>(), count, stride,
+                                      uint32_t(length), c->stream));
+    return run_var(d, c, base, c->off.as<uint64_t>(), c->len.as<uint32_t>(), inits, count,
+                   length * count, out);
+}
+
+int finish(Ctx* c, unsigned flags)
+{
+    if ((flags & MI_CRC32C_DEVICE) && (flags & MI_CRC32C_ASYNC)) return MI_CRC32C_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+}  // namespace
+
+// ==========================================================================
+extern "C" {
+
+int mi_crc32c_init(int device) { return init_device(device); }
+
+const char* mi_crc32c_strerror(int status)
+{
+    switch (status)
+    {
+        case MI_CRC32C_OK: return "ok";
+        case MI_CRC32C_EINVAL: return "invalid argument";
+        case MI_CRC32C_ENODEV: return "no usable gfx950 device";
+        case MI_CRC32C_ENOMEM: return "out of memory";
+        case MI_CRC32C_EHIP: return "HIP runtime error";
+        case MI_CRC32C_ERCCL: return "RCCL error";
+        default: return "unknown status";
+    }
+}
+
+const char* mi_crc32c_last_error(void) { return t_err.c_str(); }
+
+void* mi_crc32c_stream(void)
+{
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    return c ? static_cast<void*>(c->stream) : nullptr;
+}
+
+int mi_crc32c_stream_sync(void)
+{
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                    const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
+                    unsigned flags)
+{
+    if (count == 0) return MI_CRC32C_OK;
+    if (!offsets || !lengths || !out) return fail(MI_CRC32C_EINVAL, "null array with count > 0");
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    DeviceState* d = g_dev.load();
+    if (flags & MI_CRC32C_DEVICE)
+    {
+        if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out))) return st;
+        return finish(c, flags);
+    }
+    // Host batch: stage the spanned bytes, rebased offsets, lengths, inits.
+    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
+    for (size_t i = 0; i < count; ++i)
+    {
+        if (lengths[i] == 0) continue;
+        lo = std::min<uint64_t>(lo, offsets[i]);
+        hi = std::max<uint64_t>(hi, offsets[i] + lengths[i]);
+        total += lengths[i];
+    }
+    if (lo == UINT64_MAX) lo = hi = 0;
+    if (hi > lo && !base) return fail(MI_CRC32C_EINVAL, "null base");
+    std::vector<uint64_t> reb(count);
+    for (size_t i = 0; i < count; ++i) reb[i] = lengths[i] ? offsets[i] - lo : 0;
+    if ((st = c->data.reserve(hi - lo + 16)) || (st = c->off.reserve(count * 8)) ||
+        (st = c->len.reserve(count * 4)) || (st = c->out.reserve(count * 4)) ||
+        (inits && (st = c->inits.reserve(count * 4))))
+        return st;
+    if (hi > lo)
+        HIP_TRY(hipMemcpyAsync(c->data.p, static_cast<const uint8_t*>(base) + lo, hi - lo,
+                               hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->off.p, reb.data(), count * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->len.p, lengths, count * 4, hipMemcpyHostToDevice, c->stream));
+    if (inits)
+        HIP_TRY(hipMemcpyAsync(c->inits.p, inits, count * 4, hipMemcpyHostToDevice, c->stream));
+    if ((st = run_var(d, c, c->data.p, c->off.as<uint64_t>(), c->len.as<uint32_t>(),
+                      inits ? c->inits.as<uint32_t>() : nullptr, count, total,
+                      c->out.as<uint32_t>())))
+        return st;
+    HIP_TRY(hipMemcpyAsync(out, c->out.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
+                          const uint32_t* inits, size_t count, uint32_t* out, unsigned flags)
+{
+    if (count == 0) return MI_CRC32C_OK;
+    if (!out || (!base && length)) return fail(MI_CRC32C_EINVAL, "null pointer with count > 0");
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    DeviceState* d = g_dev.load();
+    if (flags & MI_CRC32C_DEVICE)
+    {
+        if ((st = run_fixed(d, c, base, stride, length, inits, count, out))) return st;
+        return finish(c, flags);
+    }
+    const uint64_t span = length ? (count - 1) * stride + length : 0;
+    if ((st = c->data.reserve(span + 16)) || (st = c->out.reserve(count * 4)) ||
+        (inits && (st = c->inits.reserve(count * 4))))
+        return st;
+    if (span) HIP_TRY(hipMemcpyAsync(c->data.p, base, span, hipMemcpyHostToDevice, c->stream));
+    if (inits)
+        HIP_TRY(hipMemcpyAsync(c->inits.p, inits, count * 4, hipMemcpyHostToDevice, c->stream));
+    if ((st = run_fixed(d, c, c->data.p, stride, length, inits ? c->inits.as<uint32_t>() : nullptr,
+                        count, c->out.as<uint32_t>())))
+        return st;
+    HIP_TRY(hipMemcpyAsync(out, c->out.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, unsigned flags)
+{
+    if (!out) return fail(MI_CRC32C_EINVAL, "null out");
+    if (n == 0)
+    {
+        *out = init;
+        return MI_CRC32C_OK;
+    }
+    if (!data) return fail(MI_CRC32C_EINVAL, "null data");
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    DeviceState* d = g_dev.load();
+    // Pieces of <= 1 GiB computed as one batch, chained with the combine
+    // identity crc(0, A||B) = Z_|B|(crc(0, A)) ^ crc(0, B); init goes into piece 0.
+    constexpr uint64_t kPiece = 1ull << 30;
+    const size_t np = size_t((n + kPiece - 1) / kPiece);
+    std::vector<uint64_t> off(np);
+    std::vector<uint32_t> len(np), ini(np, 0), res(np);
+    for (size_t i = 0; i < np; ++i)
+    {
+        off[i] = i * kPiece;
+        len[i] = uint32_t(std::min<uint64_t>(kPiece, n - i * kPiece));
+    }
+    ini[0] = init;
+    if (flags & MI_CRC32C_DEVICE)
+    {
+        if ((st = c->off.reserve(np * 8)) || (st = c->len.reserve(np * 4)) ||
+            (st = c->inits.reserve(np * 4)) || (st = c->out.reserve(np * 4)))
+            return st;
+        HIP_TRY(hipMemcpyAsync(c->off.p, off.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->len.p, len.data(), np * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->inits.p, ini.data(), np * 4, hipMemcpyHostToDevice, c->stream));
+        if ((st = run_var(d, c, data, c->off.as<uint64_t>(), c->len.as<uint32_t>(),
+                          c->inits.as<uint32_t>(), np, n, c->out.as<uint32_t>())))
+            return st;
+        HIP_TRY(hipMemcpyAsync(res.data(), c->out.p, np * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    else if ((st = mi_crc32c_batch(data, off.data(), len.data(), ini.data(), np, n, res.data(), 0)))
+        return st;
+    uint32_t acc = res[0];
+    for (size_t i = 1; i < np; ++i) acc = apply_zeros(d, acc, len[i]) ^ res[i];
+    *out = acc;
+    return MI_CRC32C_OK;
+}
+
+uint32_t mi_crc32c(uint32_t init, const void* data, size_t n)
+{
+    uint32_t out = 0;
+    const int st = mi_crc32c_buffer(init, data, n, &out, 0);
+    if (st != MI_CRC32C_OK)
+    {
+        std::fprintf(stderr, "consus_crc32c: GPU CRC-32C engine failed (%s): %s\n",
+                     mi_crc32c_strerror(st), t_err.c_str());
+        std::abort();
+    }
+    return out;
+}
+
+uint32_t mi_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b)
+{
+    static const Op32* ops = [] {
+        static Op32 o[64];
+        Op32 p = Op32::zero_byte();
+        for (int k = 0; k < 64; ++k)
+        {
+            o[k] = p;
+            p = p.then(p);
+        }
+        return o;
+    }();
+    uint32_t s = crc_a;
+    for (int k = 0; len_b && k < 64; ++k, len_b >>= 1)
+        if (len_b & 1u) s = ops[k].apply(s);
+    return s ^ crc_b;
+}
+
+int mi_crc32c_combine_batch(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,
+                            size_t count, uint32_t* out, unsigned flags)
+{
+    if (count == 0) return MI_CRC32C_OK;
+    if (!crc_a || !crc_b || !len_b || !out) return fail(MI_CRC32C_EINVAL, "null array");
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    DeviceState* d = g_dev.load();
+    if (flags & MI_CRC32C_DEVICE)
+    {
+        HIP_TRY(launch_combine(crc_a, crc_b, len_b, count, out, d->d_pow2, c->stream));
+        return finish(c, flags);
+    }
+    if ((st = c->inits.reserve(count * 4)) || (st = c->out.reserve(count * 4)) ||
+        (st = c->off.reserve(count * 8)) || (st = c->len.reserve(count * 4)))
+        return st;
+    HIP_TRY(hipMemcpyAsync(c->inits.p, crc_a, count * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->len.p, crc_b, count * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->off.p, len_b, count * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_combine(c->inits.as<uint32_t>(), c->len.as<uint32_t>(), c->off.as<uint64_t>(),
+                           count, c->out.as<uint32_t>(), d->d_pow2, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->out.p, count * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+// ---- streaming pipeline ----------------------------------------------------
+}  // extern "C"
+
+struct mi_crc32c_pipeline
+{
+    struct Slot
+    {
+        Ctx ctx;
+        PinBuf seg, meta, res;   // pinned: segment bytes, offsets+lengths+inits, crcs
+        DevBuf dseg, dmeta;      // device: segment bytes, offsets+lengths+inits
+        uint64_t ticket = 0;     // ticket in flight (0 = none)
+        uint32_t* host_out = nullptr;
+        size_t count = 0;
+    };
+    std::vector<Slot> slots;
+    size_t max_bytes = 0, max_records = 0;
+    uint64_t next_ticket = 1;
+    std::mutex mu;
+};
+
+namespace {
+
+int slot_complete(mi_crc32c_pipeline::Slot& s)
+{
+    if (!s.ticket) return MI_CRC32C_OK;
+    HIP_TRY(hipEventSynchronize(s.ctx.done));
+    if (s.host_out && s.count) std::memcpy(s.host_out, s.res.p, s.count * 4);
+    s.ticket = 0;
+    s.host_out = nullptr;
+    return MI_CRC32C_OK;
+}
+
+bool is_pinned(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mi_crc32c_pipeline_create(size_t max_segment_bytes, size_t max_records, int depth,
+                              mi_crc32c_pipeline** out)
+{
+    if (!out || depth < 1 || depth > 16 || max_records == 0)
+        return fail(MI_CRC32C_EINVAL, "bad pipeline arguments");
+    int st = 0;
+    DeviceState* d = dev_or_init(&st);
+    if (!d) return st;
+    auto* p = new mi_crc32c_pipeline;
+    p->slots.resize(size_t(depth));
+    p->max_bytes = max_segment_bytes;
+    p->max_records = max_records;
+    for (auto& s : p->slots)
+    {
+        if ((st = s.ctx.open(d->ordinal)) || (st = s.seg.reserve(max_segment_bytes + 16)) ||
+            (st = s.meta.reserve(max_records * 16)) || (st = s.res.reserve(max_records * 4)) ||
+            (st = s.dseg.reserve(max_segment_bytes + 16)) ||
+            (st = s.dmeta.reserve(max_records * 16)) || (st = s.ctx.out.reserve(max_records * 4)))
+        {
+            mi_crc32c_pipeline_destroy(p);
+            return st;
+        }
+    }
+    *out = p;
+    return MI_CRC32C_OK;
+}
+
+int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, size_t bytes,
+                              const uint64_t* offsets, const uint32_t* lengths,
+                              const uint32_t* inits, size_t count, uint32_t* host_out,
+                              uint64_t* ticket)
+{
+    if (!p || bytes > p->max_bytes || count > p->max_records || (count && (!offsets || !lengths)))
+        return fail(MI_CRC32C_EINVAL, "segment exceeds pipeline limits");
+    std::lock_guard<std::mutex> lock(p->mu);
+    DeviceState* d = g_dev.load();
+    const uint64_t t = p->next_ticket++;
+    auto& s = p->slots[t % p->slots.size()];
+    int st;
+    if ((st = slot_complete(s))) return st;
+    uint64_t total = 0;
+    for (size_t i = 0; i < count; ++i)
+    {
+        if (lengths[i] && offsets[i] + lengths[i] > bytes)
+            return fail(MI_CRC32C_EINVAL, "record outside segment");
+        total += lengths[i];
+    }
+    const void* src = host_segment;
+    if (bytes && !is_pinned(host_segment))
+    {
+        std::memcpy(s.seg.p, host_segment, bytes);
+        src = s.seg.p;
+    }
+    uint8_t* meta = s.meta.as<uint8_t>();
+    std::memcpy(meta, offsets, count * 8);
+    std::memcpy(meta + count * 8, lengths, count * 4);
+    if (inits) std::memcpy(meta + count * 12, inits, count * 4);
+    Ctx& c = s.ctx;
+    if (bytes) HIP_TRY(hipMemcpyAsync(s.dseg.p, src, bytes, hipMemcpyHostToDevice, c.stream));
+    HIP_TRY(hipMemcpyAsync(s.dmeta.p, meta, count * (inits ? 16 : 12), hipMemcpyHostToDevice,
+                           c.stream));
+    uint8_t* dm = s.dmeta.as<uint8_t>();
+    if ((st = run_var(d, &c, s.dseg.p, reinterpret_cast<uint64_t*>(dm),
+                      reinterpret_cast<uint32_t*>(dm + count * 8),
+                      inits ? reinterpret_cast<uint32_t*>(dm + count * 12) : nullptr, count, total,
+                      c.out.as<uint32_t>())))
+        return st;
+    HIP_TRY(hipMemcpyAsync(s.res.p, c.out.p, count * 4, hipMemcpyDeviceToHost, c.stream));
+    HIP_TRY(hipEventRecord(c.done, c.stream));
+    s.ticket = t;
+    s.host_out = host_out;
+    s.count = count;
+    if (ticket) *ticket = t;
+    return MI_CRC32C_OK;
+}
+
+int mi_crc32c_pipeline_wait(mi_crc32c_pipeline* p, uint64_t ticket)
+{
+    if (!p) return fail(MI_CRC32C_EINVAL, "null pipeline");
+    std::lock_guard<std::mutex> lock(p->mu);
+    auto& s = p->slots[ticket % p->slots.size()];
+    if (s.ticket != ticket) return MI_CRC32C_OK;  // already completed
+    return slot_complete(s);
+}
+
+int mi_crc32c_pipeline_destroy(mi_crc32c_pipeline* p)
+{
+    if (!p) return MI_CRC32C_OK;
+    int rc = MI_CRC32C_OK;
+    for (auto& s : p->slots)
+    {
+        if (s.ctx.stream)
+        {
+            if (s.ticket) rc = slot_complete(s);
+            (void)hipStreamSynchronize(s.ctx.stream);
+        }
+        for (DevBuf* b : {&s.ctx.data, &s.ctx.off, &s.ctx.len, &s.ctx.inits, &s.ctx.out,
+                          &s.ctx.items, &s.ctx.partial, &s.ctx.full_pos, &s.ctx.head_pos,
+                          &s.ctx.blk, &s.dseg, &s.dmeta})
+            if (b->p) (void)hipFree(b->p);
+        for (PinBuf* b : {&s.ctx.pin_small, &s.seg, &s.meta, &s.res})
+            if (b->p) (void)hipHostFree(b->p);
+        if (s.ctx.ev0) (void)hipEventDestroy(s.ctx.ev0);
+        if (s.ctx.ev1) (void)hipEventDestroy(s.ctx.ev1);
+        if (s.ctx.done) (void)hipEventDestroy(s.ctx.done);
+        if (s.ctx.stream) (void)hipStreamDestroy(s.ctx.stream);
+    }
+    delete p;
+    return rc;
+}
+
+// ---- memory helpers ---------------------------------------------------------
+int mi_dev_malloc(void** p, size_t bytes)
+{
+    int st = 0;
+    if (!p) return fail(MI_CRC32C_EINVAL, "null out pointer");
+    if (!dev_or_init(&st)) return st;
+    HIP_TRY(hipSetDevice(g_dev.load()->ordinal));
+    if (hipMalloc(p, std::max<size_t>(bytes, 1)) != hipSuccess)
+        return fail(MI_CRC32C_ENOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed");
+    return MI_CRC32C_OK;
+}
+
+int mi_dev_free(void* p)
+{
+    if (p) HIP_TRY(hipFree(p));
+    return MI_CRC32C_OK;
+}
+
+int mi_host_malloc_pinned(void** p, size_t bytes)
+{
+    int st = 0;
+    if (!p) return fail(MI_CRC32C_EINVAL, "null out pointer");
+    if (!dev_or_init(&st)) return st;
+    if (hipHostMalloc(p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess)
+        return fail(MI_CRC32C_ENOMEM, "hipHostMalloc(" + std::to_string(bytes) + ") failed");
+    return MI_CRC32C_OK;
+}
+
+int mi_host_free_pinned(void* p)
+{
+    if (p) HIP_TRY(hipHostFree(p));
+    return MI_CRC32C_OK;
+}
+
+int mi_memcpy(void* dst, const void* src, size_t bytes, int kind)
+{
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    const hipMemcpyKind k = kind == MI_MEMCPY_H2D   ? hipMemcpyHostToDevice
+                            : kind == MI_MEMCPY_D2H ? hipMemcpyDeviceToHost
+                                                    : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_memset(void* dev, int value, size_t bytes)
+{
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    HIP_TRY(hipMemsetAsync(dev, value, bytes, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t byte_offset)
+{
+    if ((uintptr_t(dev) & 7u) || (byte_offset & 7u))
+        return fail(MI_CRC32C_EINVAL, "fill needs 8-byte alignment");
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    HIP_TRY(launch_fill_splitmix(dev, nbytes, seed, byte_offset, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_timer_start(void)
+{
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_timer_stop(float* elapsed_ms)
+{
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (elapsed_ms) *elapsed_ms = ms;
+    return MI_CRC32C_OK;
+}
+
+// ---- RCCL ---------------------------------------------------------------------
+static ncclComm_t g_comm = nullptr;
+
+int mi_comm_unique_id(unsigned char id[MI_COMM_ID_BYTES])
+{
+    static_assert(sizeof(ncclUniqueId) <= MI_COMM_ID_BYTES, "unique id size");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(MI_CRC32C_ERCCL, ncclGetErrorString(r));
+    std::memset(id, 0, MI_COMM_ID_BYTES);
+    std::memcpy(id, &u, sizeof(u));
+    return MI_CRC32C_OK;
+}
+
+int mi_comm_init(const unsigned char id[MI_COMM_ID_BYTES], int nranks, int rank)
+{
+    int st = 0;
+    if (!thread_ctx(&st)) return st;
+    if (g_comm) return fail(MI_CRC32C_EINVAL, "communicator already initialised");
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    const ncclResult_t r = ncclCommInitRank(&g_comm, nranks, u, rank);
+    if (r != ncclSuccess) return fail(MI_CRC32C_ERCCL, ncclGetErrorString(r));
+    return MI_CRC32C_OK;
+}
+
+int mi_comm_allgather_u32(const uint32_t* dev_send, size_t count, uint32_t* dev_recv)
+{
+    int st = 0;
+    Ctx* c = thread_ctx(&st);
+    if (!c) return st;
+    if (!g_comm) return fail(MI_CRC32C_EINVAL, "no communicator");
+    const ncclResult_t r = ncclAllGather(dev_send, dev_recv, count, ncclUint32, g_comm, c->stream);
+    if (r != ncclSuccess) return fail(MI_CRC32C_ERCCL, ncclGetErrorString(r));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_comm_destroy(void)
+{
+    if (g_comm)
+    {
+        ncclCommDestroy(g_comm);
+        g_comm = nullptr;
+    }
+    return MI_CRC32C_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+/* include/consus_crc32c.h -- C ABI of the MI355X CRC-32C engine
+ * (libconsus_crc32c.so).
+ *
+ * This is the drop-in boundary for Consus's durable-log checksum path.  Every
+ * entry point computes exactly what consus::crc32c computes
+ * (common/crc32c.h:40-41, common/crc32c.cc:122-126): reflected CRC-32C
+ * (Castagnoli, poly 0x82F63B78), `init` is a previous CRC *output* (pre- and
+ * post-inverted), n == 0 returns init.  Results are bit-identical to the
+ * reference on every input.  The checksums themselves are always computed by
+ * the HIP kernels on the GPU; there is no CPU fallback.  If the engine cannot
+ * run, status-returning calls return a negative status and the drop-in
+ * `mi_crc32c` / `consus::crc32c` abort with a message (they cannot return an
+ * error under the reference's signature).
+ *
+ * Plain C types only; the caller owns every buffer.  Pointers are host
+ * pointers unless MI_CRC32C_DEVICE is passed, in which case every pointer
+ * argument of that call is a device pointer on the engine's device.  All
+ * calls are thread-safe: each calling thread gets its own HIP stream and
+ * workspaces.
+ */
+#ifndef CONSUS_CRC32C_H
+#define CONSUS_CRC32C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define MI_CRC32C_OK 0
+#define MI_CRC32C_EINVAL (-22)  /* bad argument (null pointer with count > 0, ...) */
+#define MI_CRC32C_ENODEV (-19)  /* no usable gfx950 device */
+#define MI_CRC32C_ENOMEM (-12)  /* device or pinned allocation failed */
+#define MI_CRC32C_EHIP (-5)     /* a HIP runtime call failed; see mi_crc32c_last_error() */
+#define MI_CRC32C_ERCCL (-71)   /* an RCCL call failed */
+
+/* ---- flags -------------------------------------------------------------- */
+#define MI_CRC32C_DEVICE 0x1u   /* pointer arguments are device pointers */
+#define MI_CRC32C_ASYNC 0x2u    /* DEVICE only: return once enqueued on the
+                                   calling thread's stream (mi_crc32c_stream_sync) */
+
+/* ---- engine ------------------------------------------------------------- */
+/* Select the device and upload the operator tables.  Idempotent; called
+ * implicitly with device 0 by the first compute call.
+ * replaces: the static-init dispatch choose_crc32c (common/crc32c.cc:101-120) */
+int mi_crc32c_init(int device);
+const char* mi_crc32c_strerror(int status);
+/* Message of the last failure on the calling thread ("" if none). */
+const char* mi_crc32c_last_error(void);
+/* The HIP stream (hipStream_t) the calling thread's work is enqueued on. */
+void* mi_crc32c_stream(void);
+int mi_crc32c_stream_sync(void);
+
+/* ---- the drop-in -------------------------------------------------------- */
+/* Same signature and semantics as consus::crc32c
+ * replaces: uint32_t consus::crc32c(uint32_t init, const unsigned char* data, size_t n)
+ *           common/crc32c.h:40-41, common/crc32c.cc:122-126 */
+uint32_t mi_crc32c(uint32_t init, const void* data, size_t n);
+
+/* Status-returning single-buffer form; `data` host or device per flags,
+ * `out` always a host pointer. */
+int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, unsigned flags);
+
+/* ---- batches: the durable-log record-batching path ---------------------- */
+/* Record i is the byte range [base + offsets[i], base + offsets[i] + lengths[i]);
+ * out[i] = consus::crc32c(inits ? inits[i] : 0, that range).
+ * Ranges may be unaligned, empty, unordered or overlapping.  total_bytes is
+ * the sum of lengths if the caller knows it (0 = unknown: with DEVICE arrays
+ * the engine then reads the plan size back once).
+ * replaces: the per-record call pair crc32c(crc32c(0, header, 16), entry, n)
+ *           in durable_log::append, txman/durable_log.cc:215-218 */
+int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                    const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
+                    unsigned flags);
+
+/* Fixed-stride records: record i = [base + i*stride, +length). */
+int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
+                          const uint32_t* inits, size_t count, uint32_t* out, unsigned flags);
+
+/* crc32c(0, A || B) from crc_a = crc32c(0, A), crc_b = crc32c(0, B) and |B|
+ * (the chaining identity of common/crc32c.cc:122-126).  Pure operator math. */
+uint32_t mi_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+int mi_crc32c_combine_batch(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,
+                            size_t count, uint32_t* out, unsigned flags);
+
+/* ---- streaming host segments (H2D -> CRC -> D2H overlapped) ------------- */
+/* A pipeline of `depth` slots, each with pinned staging for one segment of
+ * up to max_segment_bytes and max_records records, on its own HIP stream.
+ * submit() copies the segment into pinned staging, enqueues
+ * H2D + kernels + D2H of the CRCs and returns a ticket; wait() blocks until
+ * that ticket's CRCs are in host_out.  Submitting into a busy slot waits for
+ * that slot's previous ticket first. */
+typedef struct mi_crc32c_pipeline mi_crc32c_pipeline;
+int mi_crc32c_pipeline_create(size_t max_segment_bytes, size_t max_records, int depth,
+                              mi_crc32c_pipeline** out);
+int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, size_t bytes,
+                              const uint64_t* offsets, const uint32_t* lengths,
+                              const uint32_t* inits, size_t count, uint32_t* host_out,
+                              uint64_t* ticket);
+int mi_crc32c_pipeline_wait(mi_crc32c_pipeline* p, uint64_t ticket);
+int mi_crc32c_pipeline_destroy(mi_crc32c_pipeline* p);
+
+/* ---- device memory and synthetic inputs --------------------------------- */
+/* For callers without their own allocator (tests, bench, the durable log). */
+int mi_dev_malloc(void** p, size_t bytes);
+int mi_dev_free(void* p);
+int mi_host_malloc_pinned(void** p, size_t bytes);
+int mi_host_free_pinned(void* p);
+#define MI_MEMCPY_H2D 1
+#define MI_MEMCPY_D2H 2
+#define MI_MEMCPY_D2D 3
+int mi_memcpy(void* dst, const void* src, size_t bytes, int kind); /* synchronous */
+int mi_memset(void* dev, int value, size_t bytes);
+/* bytes [byte_offset, byte_offset + nbytes) of the splitmix64 stream of `seed`
+ * (SURVEY.md 8(d)); dev 8-byte aligned, byte_offset a multiple of 8. */
+int mi_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t byte_offset);
+
+/* ---- timing on the calling thread's stream ------------------------------ */
+int mi_timer_start(void);
+int mi_timer_stop(float* elapsed_ms); /* synchronizes the stream */
+
+/* ---- multi-GPU: RCCL over xGMI ------------------------------------------ */
+#define MI_COMM_ID_BYTES 128
+int mi_comm_unique_id(unsigned char id[MI_COMM_ID_BYTES]);
+int mi_comm_init(const unsigned char id[MI_COMM_ID_BYTES], int nranks, int rank);
+/* recv[r * count + i] = send_of_rank_r[i]; device pointers, calling thread's stream */
+int mi_comm_allgather_u32(const uint32_t* dev_send, size_t count, uint32_t* dev_recv);
+int mi_comm_destroy(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CONSUS_CRC32C_H */

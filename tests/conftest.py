@@ -1,0 +1,39 @@
+"""pytest configuration: the `gpu` marker and shared fixtures.
+
+`-m "not gpu"` runs here (no GPU): oracle vs golden vectors, host logic, the
+C-ABI library loading/exports.  `-m gpu` runs on the MI355X box: parity of
+the HIP kernels against the oracle through the C ABI.
+"""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle.oracle import Oracle
+    return Oracle()
+
+
+@pytest.fixture(scope="session")
+def reference():
+    from oracle.oracle import Reference, reference_available
+    if not reference_available():
+        pytest.skip("oracle/_ref/libref_crc32c.so not built")
+    return Reference()
+
+
+@pytest.fixture(scope="session")
+def engine():
+    import consus_amd
+    consus_amd.init(0)
+    return consus_amd

@@ -1,0 +1,27 @@
+"""Quick device-resident throughput probe for the fixed kernel (dev tool)."""
+import sys, time, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import consus_amd as E
+
+count = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+L = 4096
+E.init(0)
+data = E.DeviceBuffer(count * L)
+out = E.DeviceBuffer(count * 4)
+data.fill_splitmix64(0xC0DE)
+for _ in range(3):
+    E.device_batch_fixed(data, L, L, count, out)
+times = []
+for _ in range(20):
+    E.timer_start()
+    E.device_batch_fixed(data, L, L, count, out, asynchronous=True)
+    times.append(E.timer_stop())
+crcs = out.download(np.uint32, count)
+sys.path.insert(0, '.')
+from oracle.oracle import Oracle
+d, x = Oracle().digest(crcs)
+ms = float(np.median(times))
+gb = count * L / 1e9
+print(f"count={count} median {ms:.4f} ms min {min(times):.4f} -> {gb/ms*1e3:.1f} GB/s "
+      f"({count*L/2**30/ms*1e3:.1f} GiB/s)  digest {d:#010x} xor {x:#010x} first {crcs[0]:#010x}")
