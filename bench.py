@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident CRC-32C throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--records-per-rank R]
+
+A "step" is one pass of the hot path -- consus::crc32c over every record of
+one batch (common/crc32c.cc:122-126, the per-record call of
+txman/durable_log.cc:215-218) -- done by the HIP kernels through the C ABI
+(include/consus_crc32c.h, mi_crc32c_batch_fixed with MI_CRC32C_DEVICE).
+
+Workload (N=1): BASELINE.json configs[1] -- 1M x 4 KiB records resident in
+HBM, bytes = splitmix64 stream of seed 0xC0DE, generated on
+the device before timing.  N>1 (torchrun, one process per GPU): every rank
+owns its own 1M-record shard of the same global stream (record offset
+rank*R), so per-GPU work is fixed ("scaling": "weak") and no collective runs
+inside the timed region (records are independent).  After
+timing, every rank's CRC vector is reduced on its GPU to a digest; the
+digests are compared with the committed golden values (tests/golden).
+
+The JSON line also carries
+  roofline      algorithmic bytes per launch (sum of record lengths) / the
+                launch's average duration from HIP events on the engine's
+                stream, against the MI355X HBM3E peak (8 TB/s); `traffic` =
+                2 x FETCH_SIZE from a separate rocprofv3 --pmc pass (gfx950
+                reports half of wide streaming reads, MI355X_MICROARCH.md HBM)
+  cpu_baseline  the reference common/crc32c.cc itself (oracle/_ref, compiled
+                unmodified) on the host cores, over a bounded sample of the
+                same records (rank 0, N=1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "GiB/s CRC32C over device-resident 4 KiB records; % of HBM read peak"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E datasheet peak (MI355X_MICROARCH.md)
+SEED = 0xC0DE
+RECORD = 4096
+KERNEL_NAME = "crc32c_fixed_kernel"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--records-per-rank", type=int, default=1 << 20)
+    ap.add_argument("--record-bytes", type=int, default=RECORD)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="wall budget of each CPU-baseline leg (single, all-threads)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+def golden_digests():
+    p = os.path.join(REPO, "tests", "golden", "digests.json")
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        return json.load(f)
+
+
+# ---- HBM traffic from a separate rocprofv3 --pmc pass ---------------------------
+def pmc_traffic(args) -> tuple[float | None, str]:
+    """Run this script under `rocprofv3 --pmc FETCH_SIZE` (its own pass, no
+    tracing domains) and return corrected HBM read bytes per launch."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not found"
+    out = tempfile.mkdtemp(prefix="pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc",
+           "--", sys.executable, os.path.abspath(__file__), "--child-pmc",
+           "--records-per-rank", str(args.records_per_rank),
+           "--record-bytes", str(args.record_bytes)]
+    try:
+        subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL,
+                       stderr=subprocess.DEVNULL, cwd=out)
+    except Exception as e:  # noqa: BLE001 -- traffic is optional, the bench is not
+        return None, f"rocprofv3 pass failed: {e}"
+    vals = []
+    for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if KERNEL_NAME in row.get("Kernel_Name", "") and \
+                        row.get("Counter_Name") == "FETCH_SIZE":
+                    vals.append(float(row["Counter_Value"]))
+    shutil.rmtree(out, ignore_errors=True)
+    if not vals:
+        return None, "no FETCH_SIZE rows for the kernel"
+    # FETCH_SIZE is in KiB; gfx950 tallies 128-B requests of wide streaming
+    # reads at 64 B, so double it (MI355X_MICROARCH.md, HBM).
+    return 2.0 * 1024.0 * float(np.median(vals)), f"{len(vals)} dispatches, median, x2 gfx950 correction"
+
+
+# ---- CPU baseline: the reference itself ---------------------------------------
+def cpu_baseline(args) -> dict:
+    from oracle.oracle import Oracle, Reference, reference_available
+    if not reference_available():
+        return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference",
+                "sample": "oracle/_ref/libref_crc32c.so not built"}
+    ref, orc = Reference(), Oracle()
+    L = args.record_bytes
+    n = (256 << 20) // L                       # 256 MiB sample of the same records
+    buf = orc.fill(n * L, SEED, 0)
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                         else os.cpu_count() or 1))
+
+    def rate(th):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            ref.fixed(buf, L, L, n, threads=th)
+            passes += 1
+            dt = time.perf_counter() - t0
+            if dt >= args.cpu_seconds:
+                return passes * n * L / dt / 2**30, passes
+    crc_ref = ref.fixed(buf, L, L, 64, threads=1)
+    single, p1 = rate(1)
+    multi, pm = rate(threads)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(multi, 2), "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "single_thread_value": round(single, 2),
+            "sample": f"first {n} of the same {L}-B records (256 MiB, host memory), "
+                      f"consus::crc32c from common/crc32c.cc compiled unmodified "
+                      f"(dispatch {'sse42 crc32q' if ref.lib.ref_dispatch_is_sse42() else 'slicing-by-8'}), "
+                      f"{p1} passes single-thread + {pm} passes x {threads} std::threads, "
+                      f"cpu: {model}",
+            "first_crc": int(crc_ref[0])}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not args.child_pmc:
+        if world == 1 and args.gpus > 1:
+            sys.exit("for --gpus N>1 launch with torch.distributed.run (one process per GPU)")
+
+    # Traffic pass first, before this process touches the GPU.
+    traffic, traffic_note = (None, "skipped")
+    if rank == 0 and world == 1 and not args.child_pmc and not args.no_pmc:
+        traffic, traffic_note = pmc_traffic(args)
+
+    # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.
+    import consus_amd as E
+    E.init(local)
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    R, L = args.records_per_rank, args.record_bytes
+    data = E.DeviceBuffer(R * L)
+    out = E.DeviceBuffer(R * 4)
+    data.fill_splitmix64(SEED, byte_offset=rank * R * L)
+
+    if args.child_pmc:
+        for _ in range(3):
+            E.device_batch_fixed(data, L, L, R, out)
+        return
+
+    for _ in range(args.warmup):
+        E.device_batch_fixed(data, L, L, R, out)
+    E.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    E.sync()
+    t0 = time.perf_counter()
+    E.timer_start()
+    for _ in range(args.steps):
+        E.device_batch_fixed(data, L, L, R, out, asynchronous=True)
+    ev_ms = E.timer_stop()          # HIP events on the launch stream (synchronizes it)
+    E.sync()
+    barrier()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([wall, ev_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, ev_ms_max = float(t[0]), float(t[1])
+    else:
+        ev_ms_max = ev_ms
+
+    # Digest of this rank's CRC vector, computed on the GPU: crc32c(0, LE bytes).
+    crcs_dev_digest = E.crc32c_device(out, R * 4)
+    digests = [crcs_dev_digest]
+    if dist is not None:
+        g = [None] * world
+        dist.all_gather_object(g, crcs_dev_digest)
+        digests = g
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    gold = golden_digests().get(f"fixed_{L}_seed{SEED:#x}_per_{R}", {})
+    verified = None
+    if gold:
+        exp = gold.get("block_digests", [])
+        verified = all(i < len(exp) and digests[i] == exp[i] for i in range(world))
+
+    total_bytes = world * R * L * args.steps
+    value = total_bytes / wall / 2**30
+    per_launch_ms = ev_ms / args.steps
+    achieved = R * L / (per_launch_ms * 1e-3) / 1e9
+    rec = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: splitmix64(0xC0DE ^ word) stream, generated in HBM before timing "
+                "(SURVEY.md 8(d))",
+        "config": {
+            "workload": f"{R} x {L} B records, device-resident, {world} x MI355X "
+                        f"(BASELINE.json configs[1] per GPU)",
+            "records_per_rank": R, "record_bytes": L, "global_batch": world * R,
+            "parallelism": f"record shards x{world}, no collective in the timed region",
+        },
+        "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None if traffic is None else round(traffic),
+            "algorithmic_bytes": R * L, "kernel": KERNEL_NAME,
+            "launch_ms": round(per_launch_ms, 4), "traffic_note": traffic_note,
+        },
+        "digest_verified": verified,
+        "digests": [f"{d:#010x}" for d in digests],
+    }
+    if world > 1:
+        rec["roofline"]["launch_ms_max_over_ranks"] = round(ev_ms_max / args.steps, 4)
+    if world == 1 and not args.no_cpu:
+        rec["cpu_baseline"] = cpu_baseline(args)
+    else:
+        rec["cpu_baseline"] = None
+    print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

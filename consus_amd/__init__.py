@@ -84,6 +84,7 @@ _SIGS = {
     "mi_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "mi_comm_allgather_u32": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
     "mi_comm_destroy": (C.c_int, []),
+    "mi_workload_zipf_lengths": (None, [C.c_uint64, C.c_uint64, C.c_size_t, C.c_void_p]),
 }
 
 _lib = None
@@ -135,6 +136,23 @@ def crc32c(init_crc: int, data, n: int | None = None) -> int:
     _check(lib().mi_crc32c_buffer(init_crc & 0xFFFFFFFF, C.c_void_p(a.ctypes.data), n,
                                   C.byref(out), 0), "mi_crc32c_buffer")
     return int(out.value)
+
+
+def crc32c_device(buf: "DeviceBuffer", nbytes: int | None = None, init_crc: int = 0,
+                  offset: int = 0) -> int:
+    """consus::crc32c(init, device bytes [offset, offset + nbytes)) on the GPU."""
+    n = buf.nbytes - offset if nbytes is None else nbytes
+    out = C.c_uint32(0)
+    _check(lib().mi_crc32c_buffer(init_crc & 0xFFFFFFFF, C.c_void_p(buf.ptr + offset), n,
+                                  C.byref(out), FLAG_DEVICE), "mi_crc32c_buffer")
+    return int(out.value)
+
+
+def zipf_lengths(seed: int, count: int, first: int = 0) -> np.ndarray:
+    """Config-3 record lengths (workload.cc); host-only, no device needed."""
+    out = np.zeros(count, dtype=np.uint32)
+    lib().mi_workload_zipf_lengths(seed, first, count, C.c_void_p(out.ctypes.data))
+    return out
 
 
 def crc32c_batch(buf, offsets, lengths, inits=None) -> np.ndarray:

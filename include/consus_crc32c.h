@@ -117,6 +117,10 @@ int mi_memset(void* dev, int value, size_t bytes);
  * (SURVEY.md 8(d)); dev 8-byte aligned, byte_offset a multiple of 8. */
 int mi_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t byte_offset);
 
+/* Host-side synthetic record lengths of BASELINE.json config 3 (Zipf 64 B -
+ * 64 KiB; definition in consus_amd/csrc/workload.cc).  No device needed. */
+void mi_workload_zipf_lengths(uint64_t seed, uint64_t first, size_t count, uint32_t* out);
+
 /* ---- timing on the calling thread's stream ------------------------------ */
 int mi_timer_start(void);
 int mi_timer_stop(float* elapsed_ms); /* synchronizes the stream */

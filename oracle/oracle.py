@@ -153,9 +153,20 @@ class Reference(_Lib):
         L.ref_crc32c_batch_mt.restype = None
         L.ref_crc32c_batch_mt.argtypes = [C.c_void_p, _u64p, _u32p, _u32p, C.c_size_t, _u32p,
                                           C.c_int]
+        L.ref_crc32c_splitmix_var.restype = None
+        L.ref_crc32c_splitmix_var.argtypes = [C.c_uint64, _u64p, _u32p, C.c_size_t, _u32p,
+                                              C.c_int]
         L.ref_crc32c_splitmix_fixed.restype = None
         L.ref_crc32c_splitmix_fixed.argtypes = [C.c_uint64, C.c_size_t, C.c_uint64, C.c_size_t,
                                                 _u32p, C.c_int]
+
+    def splitmix_var(self, seed: int, offsets, lengths, threads: int = 8) -> np.ndarray:
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        out = np.zeros(off.size, dtype=np.uint32)
+        self.lib.ref_crc32c_splitmix_var(seed, _ptr(off, _u64p), _ptr(ln, _u32p), off.size,
+                                         _ptr(out, _u32p), threads)
+        return out
 
     def crc32c(self, init: int, data, n: int | None = None, offset: int = 0,
                impl: str = "api") -> int:

@@ -111,3 +111,21 @@ REF_EXPORT void ref_crc32c_splitmix_fixed(uint64_t seed, size_t rec_len, uint64_
         }
     });
 }
+
+// Per-record CRCs of records [base_off + offsets[i], +lengths[i]) of the
+// splitmix64 stream `seed` (config 3: packed Zipf-length records), generated
+// on the fly per record.
+REF_EXPORT void ref_crc32c_splitmix_var(uint64_t seed, const uint64_t* offsets,
+                                        const uint32_t* lengths, size_t count, uint32_t* out,
+                                        int threads)
+{
+    parallel_ranges(count, threads, [=](size_t lo, size_t hi) {
+        std::vector<unsigned char> buf;
+        for (size_t i = lo; i < hi; ++i)
+        {
+            if (buf.size() < lengths[i] + size_t(8)) buf.resize(lengths[i] + size_t(8));
+            oracle_fill_stream(buf.data(), lengths[i], seed, offsets[i]);
+            out[i] = consus::crc32c(0, buf.data(), lengths[i]);
+        }
+    });
+}
