@@ -22,6 +22,14 @@
 
 #include "crc32c_kernels.h"
 
+// Ablation modes for tools/ablate.py (the product build is mode 0):
+//   1 = skip the LDS table staging, 2 = no global loads (synthetic data),
+//   4 = no table lookups (data XORed straight into the chains).
+// Results are wrong in any mode != 0; only the timing is meaningful.
+#ifndef MI_CRC_ABLATE
+#define MI_CRC_ABLATE 0
+#endif
+
 namespace mi_crc {
 
 extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -36,12 +44,20 @@ __device__ __forceinline__ uint32_t lds32(uint32_t byte_addr)
     return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(byte_addr));
 }
 
+// a ^ b ^ c in one CDNA4 v_bitop3_b32 (truth table 0x96); hipcc does not
+// form it from two v_xor_b32 by itself.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // Stage the table image into LDS: G^{128} replicated 32x bank-private, then
 // T_0..T_15, G^{32}, G^{64} verbatim.  Byte address of G^{128}_t[b] for the
 // lane whose ds_read_b32 group position is c (= lane & 31):
 //   (t >> 1) * 65536 + b * 256 + (t & 1) * 128 + c * 4   ->  bank == c.
 __device__ __forceinline__ void stage_tables(const uint32_t* __restrict__ g)
 {
+    if (MI_CRC_ABLATE & 1) return;
     for (uint32_t i = threadIdx.x; i < 1024u * 8u; i += blockDim.x)
     {
         const uint32_t e = i >> 3;          // t * 256 + b
@@ -75,15 +91,17 @@ template <int M>
 __device__ __forceinline__ uint32_t zT(uint32_t v)
 {
     constexpr uint32_t k0 = kLdsT + (4 * M - 1) * 1024;
-    return lds32(k0 + ((v & 0xFFu) << 2)) ^ lds32(k0 - 1024 + ((v >> 6) & 0x3FCu)) ^
-           lds32(k0 - 2048 + ((v >> 14) & 0x3FCu)) ^ lds32(k0 - 3072 + ((v >> 22) & 0x3FCu));
+    return xor3(lds32(k0 + ((v & 0xFFu) << 2)), lds32(k0 - 1024 + ((v >> 6) & 0x3FCu)),
+                lds32(k0 - 2048 + ((v >> 14) & 0x3FCu))) ^
+           lds32(k0 - 3072 + ((v >> 22) & 0x3FCu));
 }
 
 // Z_n(v) from a G^n table set at LDS byte offset `base` (byte j uses G_j).
 __device__ __forceinline__ uint32_t zG(uint32_t base, uint32_t v)
 {
-    return lds32(base + ((v & 0xFFu) << 2)) ^ lds32(base + 1024 + ((v >> 6) & 0x3FCu)) ^
-           lds32(base + 2048 + ((v >> 14) & 0x3FCu)) ^ lds32(base + 3072 + ((v >> 22) & 0x3FCu));
+    return xor3(lds32(base + ((v & 0xFFu) << 2)), lds32(base + 1024 + ((v >> 6) & 0x3FCu)),
+                lds32(base + 2048 + ((v >> 14) & 0x3FCu))) ^
+           lds32(base + 3072 + ((v >> 22) & 0x3FCu));
 }
 
 // One 128-B row: each lane folds its 16 bytes into its four chains.
@@ -91,6 +109,14 @@ __device__ __forceinline__ uint32_t zG(uint32_t base, uint32_t v)
 // conflict-free ds_read_b32 in flight per row.
 __device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint32_t li)
 {
+    if (MI_CRC_ABLATE & 4)
+    {
+        V[0] = (V[0] >> 1) ^ d.x;
+        V[1] = (V[1] >> 1) ^ d.y;
+        V[2] = (V[2] >> 1) ^ d.z;
+        V[3] = (V[3] >> 1) ^ d.w;
+        return;
+    }
     uint32_t a[16], r[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -102,10 +128,10 @@ __device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) r[i] = lds32(kLdsMain + a[i]);
-    V[0] = r[0] ^ r[1] ^ r[2] ^ r[3] ^ d.x;
-    V[1] = r[4] ^ r[5] ^ r[6] ^ r[7] ^ d.y;
-    V[2] = r[8] ^ r[9] ^ r[10] ^ r[11] ^ d.z;
-    V[3] = r[12] ^ r[13] ^ r[14] ^ r[15] ^ d.w;
+    V[0] = xor3(xor3(r[0], r[1], r[2]), r[3], d.x);
+    V[1] = xor3(xor3(r[4], r[5], r[6]), r[7], d.y);
+    V[2] = xor3(xor3(r[8], r[9], r[10]), r[11], d.z);
+    V[3] = xor3(xor3(r[12], r[13], r[14]), r[15], d.w);
 }
 
 // Fold a team's 32 chains into the raw CRC of the team's bytes, assuming the
@@ -120,9 +146,21 @@ __device__ __forceinline__ uint32_t team_fold(const uint32_t (&V)[4])
     return zG(kLdsZ64, w) ^ __shfl_xor(w, 4);
 }
 
+// Record bytes are read exactly once: non-temporal loads (global_load_dwordx4
+// ... nt) keep them from displacing L2/MALL lines.  Measured on MI355X with
+// this kernel's access pattern (tools/probe.py): 7.07 TB/s nt vs 6.19 TB/s
+// with default-policy loads.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint4 load16(const uint8_t* p)
 {
-    return *reinterpret_cast<const uint4*>(p);
+    if (MI_CRC_ABLATE & 2)
+    {
+        const uint32_t a = uint32_t(uintptr_t(p));
+        return make_uint4(a, a * 3u, a ^ 0x55u, a + 7u);
+    }
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 // ---------------------------------------------------------------------------
@@ -185,6 +223,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_kernel(
                 const int32_t o = col0 + int32_t(gb) * kGroupBytes + r * kRowBytes;
                 B[r] = load16(PADDED && o < 0 ? rbase : rbase + o);
             }
+            __builtin_amdgcn_sched_barrier(0);  // all 16 loads issue before any use
             // keep the init word's wait behind the data loads (no hoisting)
             if (INITS) asm volatile("" : "+v"(init_word));
             if (PADDED)
@@ -218,6 +257,74 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_kernel(
     }
 }
 
+// Software-pipelined fast path for records of exactly G KiB (G even), the
+// shape of the headline batch (4 KiB): group g+1 -- or the next record's group
+// 0 -- is in flight while group g is folded, so every wave always has 8 KiB
+// of loads outstanding.  The loop body is straight-line per record, so the
+// loop-carried buffer is the same 8 loads on every path into the header and
+// the compiler's vmcnt accounting stays exact.
+template <int G, bool INITS>
+__global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_pipe_kernel(
+    const uint8_t* __restrict__ base, uint64_t stride, const uint32_t* __restrict__ inits,
+    uint64_t init_stride, uint64_t count, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables)
+{
+    static_assert(G % 2 == 0, "buffers alternate per group");
+    stage_tables(tables);
+
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t li = lane_info();
+    const uint64_t team = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kTeam;
+    const uint64_t nteams = uint64_t(gridDim.x) * kBlock / kTeam;
+    const uint64_t team0 = team & ~uint64_t(7);
+    const uint64_t iters = team0 < count ? (count - team0 + nteams - 1) / nteams : 0;
+    if (iters == 0) return;
+
+    auto rec_of = [&](uint64_t it) {
+        const uint64_t r = team + it * nteams;
+        return r < count ? r : count - 1;
+    };
+    auto load_group = [&](uint4 (&buf)[kGroupRows], uint64_t rec, int g) {
+        const uint8_t* p = base + rec * stride + tl * 16 + g * kGroupBytes;
+#pragma unroll
+        for (int r = 0; r < kGroupRows; ++r) buf[r] = load16(p + r * kRowBytes);
+    };
+
+    uint4 A[kGroupRows], B[kGroupRows];
+    uint64_t rec = rec_of(0);
+    uint32_t init_word = INITS ? inits[rec * init_stride] : 0u;
+    load_group(A, rec, 0);
+    for (uint64_t it = 0; it < iters; ++it)
+    {
+        const uint64_t next = rec_of(it + 1);
+        uint32_t V[4] = {0, 0, 0, 0};
+        uint32_t next_init = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+        {
+            uint4(&cur)[kGroupRows] = (g % 2 == 0) ? A : B;
+            uint4(&nxt)[kGroupRows] = (g % 2 == 0) ? B : A;
+            if (g + 1 < G)
+                load_group(nxt, rec, g + 1);
+            else
+            {
+                load_group(nxt, next, 0);
+                if (INITS) next_init = inits[next * init_stride];
+            }
+            // Keep all 8 loads ahead of this group's folding (the scheduler
+            // would otherwise sink them into it to save registers).
+            __builtin_amdgcn_sched_barrier(0);
+            if (g == 0) cur[0].x ^= tl == 0 ? ~init_word : 0u;
+#pragma unroll
+            for (int r = 0; r < kGroupRows; ++r) row_update(V, cur[r], li);
+        }
+        const uint32_t raw = team_fold(V);
+        if (tl == 0 && team + it * nteams < count) out[rec] = ~raw;
+        rec = next;
+        if (INITS) init_word = next_init;
+    }
+}
+
 hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const uint32_t* inits,
                         uint64_t count, uint32_t* out, const uint32_t* tables, int grid,
                         hipStream_t stream)
@@ -228,6 +335,25 @@ hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const u
     const uint64_t need = (count + (kBlock / kTeam) - 1) / (kBlock / kTeam);
     if (uint64_t(grid) > need) grid = int(need);
     const bool padded = len != groups * kGroupBytes;
+    const uint32_t* ipp = inits ? inits : tables + kTabZero;
+    const uint64_t isp = inits ? 1 : 0;
+    const uint8_t* bp = static_cast<const uint8_t*>(base);
+#define MI_LAUNCH_PIPE(GG, I)                                                                 \
+    hipLaunchKernelGGL((crc32c_fixed_pipe_kernel<GG, I>), dim3(grid), dim3(kBlock), kLdsBytes, \
+                       stream, bp, stride, ipp, isp, count, out, tables)
+    if (!padded && (groups == 4 || groups == 2))
+    {
+        if (groups == 4 && inits)
+            MI_LAUNCH_PIPE(4, true);
+        else if (groups == 4)
+            MI_LAUNCH_PIPE(4, false);
+        else if (inits)
+            MI_LAUNCH_PIPE(2, true);
+        else
+            MI_LAUNCH_PIPE(2, false);
+        return hipGetLastError();
+    }
+#undef MI_LAUNCH_PIPE
     const uint32_t* ip = inits ? inits : zero_word;
     const uint64_t is = inits ? 1 : 0;
     const uint8_t* b = static_cast<const uint8_t*>(base);
@@ -646,7 +772,11 @@ hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const ui
 // Allow the 152 KiB dynamic LDS image on the two persistent kernels.
 hipError_t configure_kernels()
 {
-    const void* k[] = {reinterpret_cast<const void*>(&crc32c_fixed_kernel<false, false>),
+    const void* k[] = {reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<4, false>),
+                       reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<4, true>),
+                       reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<2, false>),
+                       reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<2, true>),
+                       reinterpret_cast<const void*>(&crc32c_fixed_kernel<false, false>),
                        reinterpret_cast<const void*>(&crc32c_fixed_kernel<false, true>),
                        reinterpret_cast<const void*>(&crc32c_fixed_kernel<true, false>),
                        reinterpret_cast<const void*>(&crc32c_fixed_kernel<true, true>)};

@@ -1,0 +1,101 @@
+// tools/probe.hip -- HBM read-ceiling calibration kernels (development tool,
+// not part of the product library).  Each probe reads a device buffer with a
+// given access pattern and XOR-reduces it (trivial compute), so its rate is
+// the memory-side ceiling for that pattern on this MI355X.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld(const uint4* p)
+{
+    if (NT)
+    {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *p;
+}
+
+// Contiguous: every wave-instruction reads 1 KiB contiguous; U loads in flight.
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void probe_stream(const uint4* __restrict__ p, uint64_t n16,
+                                                    uint32_t* __restrict__ sink)
+{
+    const uint64_t tid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t nth = uint64_t(gridDim.x) * blockDim.x;
+    uint32_t acc = 0;
+    uint64_t i = tid;
+    for (; i + (U - 1) * nth < n16; i += U * nth)
+    {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld<NT>(p + i + u * nth);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (; i < n16; i += nth) acc ^= ld<NT>(p + i).x;
+    if (acc == 0x12345678u) sink[tid & 1023] = acc;
+}
+
+// The fixed kernel's access pattern: 8-lane teams, 128-B rows, record stride
+// 4 KiB, 16 loads per lane per step, persistent grid of 1024-thread blocks.
+template <bool NT>
+__global__ __launch_bounds__(1024, 1) void probe_team(const uint8_t* __restrict__ base,
+                                                      uint64_t count, uint32_t* __restrict__ sink)
+{
+    const uint32_t tl = threadIdx.x & 7u;
+    const uint64_t team = (uint64_t(blockIdx.x) * 1024 + threadIdx.x) / 8;
+    const uint64_t nteams = uint64_t(gridDim.x) * 1024 / 8;
+    uint32_t acc = 0;
+    for (uint64_t rec = team; rec < count; rec += nteams)
+    {
+        const uint8_t* r = base + rec * 4096 + tl * 16;
+        for (int g = 0; g < 4; g += 2)
+        {
+            uint4 v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                v[k] = ld<NT>(reinterpret_cast<const uint4*>(r + g * 1024 + k * 128));
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+        }
+    }
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
+}  // namespace
+
+extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid, int reps,
+                           uint32_t* sink)
+{
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    const uint4* p = static_cast<const uint4*>(buf);
+    const uint64_t n16 = bytes / 16;
+    auto launch = [&] {
+        switch (which)
+        {
+            case 0: hipLaunchKernelGGL((probe_stream<false, 8>), dim3(grid), dim3(256), 0, 0, p, n16, sink); break;
+            case 1: hipLaunchKernelGGL((probe_stream<true, 8>), dim3(grid), dim3(256), 0, 0, p, n16, sink); break;
+            case 2: hipLaunchKernelGGL((probe_stream<false, 16>), dim3(grid), dim3(256), 0, 0, p, n16, sink); break;
+            case 3: hipLaunchKernelGGL((probe_team<false>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+            case 4: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+        }
+    };
+    launch();
+    hipDeviceSynchronize();
+    hipEventRecord(a, 0);
+    for (int i = 0; i < reps; ++i) launch();
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return ms / reps;
+}
