@@ -264,3 +264,77 @@ def timer_stop() -> float:
     ms = C.c_float(0)
     _check(lib().mi_timer_stop(C.byref(ms)), "mi_timer_stop")
     return float(ms.value)
+
+
+# ---- pinned host memory and the streaming pipeline -----------------------------
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc) exposed as a numpy uint8 array."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p(0)
+        _check(lib().mi_host_malloc_pinned(C.byref(p), max(int(nbytes), 1)),
+               "mi_host_malloc_pinned")
+        self.ptr = int(p.value)
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))
+
+    def free(self) -> None:
+        if self.ptr:
+            self.array = None
+            _check(lib().mi_host_free_pinned(C.c_void_p(self.ptr)), "mi_host_free_pinned")
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Pipeline:
+    """H2D -> CRC -> D2H of host segments overlapped over `depth` HIP streams
+    (mi_crc32c_pipeline_*).  Results land in `out` at wait(ticket)."""
+
+    def __init__(self, max_segment_bytes: int, max_records: int, depth: int = 2):
+        h = C.c_void_p(0)
+        _check(lib().mi_crc32c_pipeline_create(max_segment_bytes, max_records, depth,
+                                               C.byref(h)), "mi_crc32c_pipeline_create")
+        self._h = h
+        self._live: dict[int, tuple] = {}
+
+    def submit(self, segment, offsets, lengths, out: np.ndarray, inits=None,
+               nbytes: int | None = None) -> int:
+        seg = segment if isinstance(segment, PinnedBuffer) else None
+        if seg is not None:
+            ptr, n = seg.ptr, seg.nbytes if nbytes is None else nbytes
+            keep = seg
+        else:
+            a = _as_u8(segment)
+            ptr, n, keep = a.ctypes.data, a.size if nbytes is None else nbytes, a
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+        assert out.dtype == np.uint32 and out.size >= off.size and out.flags.c_contiguous
+        t = C.c_uint64(0)
+        _check(lib().mi_crc32c_pipeline_submit(self._h, C.c_void_p(ptr), n, _np_ptr(off),
+                                               _np_ptr(ln), _np_ptr(ini), off.size,
+                                               _np_ptr(out), C.byref(t)),
+               "mi_crc32c_pipeline_submit")
+        self._live[int(t.value)] = (keep, out)
+        return int(t.value)
+
+    def wait(self, ticket: int) -> None:
+        _check(lib().mi_crc32c_pipeline_wait(self._h, ticket), "mi_crc32c_pipeline_wait")
+        self._live.pop(ticket, None)
+
+    def close(self) -> None:
+        if self._h:
+            _check(lib().mi_crc32c_pipeline_destroy(self._h), "mi_crc32c_pipeline_destroy")
+            self._h = None
+            self._live.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

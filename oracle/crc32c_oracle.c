@@ -268,3 +268,15 @@ void oracle_fill(uint8_t* dst, size_t nbytes, uint64_t seed, uint64_t byte_offse
 {
     oracle_fill_stream(dst, nbytes, seed, byte_offset);
 }
+
+/* Batch-CRC callback with the signature of consus::durable_log_batch_crc /
+ * mi_dlog_batch_crc, so CPU tests can run the durable log's host logic
+ * (segments, watermark, framing, replay) with the oracle as the engine. */
+int oracle_dlog_batch(void* ctx, const void* base, const uint64_t* off, const uint32_t* len,
+                      size_t count, uint64_t total, uint32_t* out)
+{
+    (void)ctx;
+    (void)total;
+    oracle_crc32c_batch((const uint8_t*)base, off, len, NULL, count, out, 1);
+    return 0;
+}

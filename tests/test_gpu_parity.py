@@ -88,3 +88,80 @@ def test_device_fill_matches_definition(engine, oracle):
     d = engine.DeviceBuffer(1 << 20)
     d.fill_splitmix64(0xC0DE, byte_offset=4096 * 5)
     assert np.array_equal(d.download(), oracle.fill(1 << 20, 0xC0DE, 4096 * 5))
+
+
+def make_frames(rng, nbytes, max_entry=20000):
+    """A durable-log segment: [recno BE][len BE][entry][crc slot] frames."""
+    buf = bytearray()
+    offs, lens = [], []
+    recno = 1
+    while True:
+        n = int(rng.integers(0, max_entry))
+        if len(buf) + 20 + n > nbytes:
+            break
+        offs.append(len(buf))
+        lens.append(16 + n)
+        buf += recno.to_bytes(8, "big") + n.to_bytes(8, "big")
+        buf += rng.integers(0, 256, n, dtype=np.uint8).tobytes() + b"\0\0\0\0"
+        recno += 1
+    return np.frombuffer(bytes(buf), dtype=np.uint8), np.array(offs, np.uint64), \
+        np.array(lens, np.uint32)
+
+
+def test_pipeline_segments_pageable_and_pinned(engine, oracle):
+    rng = np.random.default_rng(8)
+    segs = [make_frames(rng, 4 << 20) for _ in range(5)]
+    p = engine.Pipeline(4 << 20, 4096, depth=2)
+    outs, tickets = [], []
+    pinned = engine.PinnedBuffer(4 << 20)
+    for i, (buf, off, ln) in enumerate(segs):
+        out = np.zeros(off.size, dtype=np.uint32)
+        if i % 2:
+            pinned_i = engine.PinnedBuffer(buf.size)
+            pinned_i.array[:] = buf
+            tickets.append(p.submit(pinned_i, off, ln, out))
+            outs.append((out, pinned_i))
+        else:
+            tickets.append(p.submit(buf, off, ln, out))
+            outs.append((out, None))
+    for t in tickets:
+        p.wait(t)
+    for (buf, off, ln), (out, _) in zip(segs, outs):
+        assert np.array_equal(out, oracle.batch(buf, off, ln))
+    p.close()
+    pinned.free()
+
+
+def test_device_batch_var_and_combine(engine, oracle):
+    rng = np.random.default_rng(12)
+    count = 20000
+    lengths = engine.zipf_lengths(0x5EED, count)
+    offsets = np.zeros(count, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    total = int(lengths.sum())
+    data = engine.DeviceBuffer(total + 16)
+    data.fill_splitmix64(0xDA7A5EED)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    for hint in (total, 0):
+        engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=hint)
+        got = d_out.download(np.uint32, count)
+        host = data.download(np.uint8, total)
+        assert np.array_equal(got, oracle.batch(host, offsets, lengths))
+    a = rng.integers(0, 2**32, 1000, dtype=np.uint32)
+    b = rng.integers(0, 2**32, 1000, dtype=np.uint32)
+    n = rng.integers(0, 1 << 40, 1000, dtype=np.uint64)
+    out = np.zeros(1000, dtype=np.uint32)
+    st = engine.lib().mi_crc32c_combine_batch(a.ctypes.data, b.ctypes.data, n.ctypes.data, 1000,
+                                               out.ctypes.data, 0)
+    assert st == 0
+    assert list(out) == [oracle.combine(int(x), int(y), int(z)) for x, y, z in zip(a, b, n)]
+
+
+def test_large_single_buffer(engine, oracle):
+    rng = np.random.default_rng(13)
+    buf = rng.integers(0, 256, (1 << 30) + 12345, dtype=np.uint8)
+    for n in (buf.size, (1 << 30), 3 << 28):
+        assert engine.crc32c(0x1234, buf[:n]) == oracle.crc32c(0x1234, buf, n)
