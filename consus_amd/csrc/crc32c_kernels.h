@@ -17,6 +17,8 @@ constexpr int kGroupBytes = kRowBytes * kGroupRows;  // 1 KiB
 constexpr int kChunk = 4096;                // variable-length work unit
 constexpr int kBlock = 1024;                // threads per workgroup (16 waves)
 constexpr int kSmallRecord = 32;            // records shorter than this are finished byte-serially
+constexpr uint32_t kLongChunks = 64;        // records with more full chunks take the long path
+constexpr int kLongBlock = 1024;            // threads per long record
 
 // Global table image uploaded once per device (u32 words).
 constexpr int kTabMain = 0;                 // G^{128}_j, 4 x 256  (row fold, replicated bank-private in LDS)
@@ -24,7 +26,9 @@ constexpr int kTabT = 1024;                 // T_0..T_15, 16 x 256 (slice-by-16)
 constexpr int kTabZ32 = kTabT + 4096;       // G^{32}_j
 constexpr int kTabZ64 = kTabZ32 + 1024;     // G^{64}_j
 constexpr int kTabZChunk = kTabZ64 + 1024;  // G^{4096}_j (chunk combine)
-constexpr int kTabZero = kTabZChunk + 1024;  // 4 zero words (init 0 when inits == nullptr)
+constexpr int kTabZLong = kTabZChunk + 1024;   // G^{1024*4096} (long-record stride)
+constexpr int kTabZC2 = kTabZLong + 1024;      // G^{4096*2^b}, b = 0..9
+constexpr int kTabZero = kTabZC2 + 10 * 1024;  // 4 zero words (init 0 when inits == nullptr)
 constexpr int kTabWords = kTabZero + 4;
 
 // LDS image of the record kernels (bytes).
@@ -62,6 +66,7 @@ struct VarWorkspace
     uint32_t* partial;    // capacity `item_cap`
     uint32_t* full_pos;   // count
     uint32_t* head_pos;   // count
+    uint32_t* longs;      // count (records on the long path)
     uint64_t item_cap;
 };
 
@@ -71,7 +76,8 @@ hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWor
                              const uint32_t* tables, int grid, hipStream_t stream);
 hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                                const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
-                               uint32_t* out, const uint32_t* tables, hipStream_t stream);
+                               uint32_t* out, const uint32_t* tables, const uint32_t* pow2,
+                               hipStream_t stream);
 uint32_t var_plan_blocks(uint64_t count);
 
 hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,

@@ -410,6 +410,19 @@ __device__ __forceinline__ RecShape rec_shape(uint64_t a, uint32_t L)
     return s;
 }
 
+__device__ __forceinline__ Item full_item(const RecShape& s, uint32_t rid, uint32_t j)
+{
+    // The earliest full chunk also carries init bytes when the head chunk
+    // holds fewer than 4 bytes (or there is none): record start = chunk
+    // start - rem.
+    Item it;
+    it.end = s.e - uint64_t(j) * kChunk;
+    const bool first = j + 1 == s.nfull && s.rem < 4;
+    it.len = kChunk | (first ? s.rem << kItemShiftBit : 0u);
+    it.rec_flag = rid | (first ? kItemStart : 0u);
+    return it;
+}
+
 // Block-wide exclusive scan of one u32 per thread (256 threads, 4 waves).
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t& total)
 {
@@ -490,14 +503,18 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
         if (threadIdx.x == 0) carry = c + tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) blk[n] = carry;
+    if (threadIdx.x == 0)
+    {
+        blk[n] = carry;    // total items
+        blk[n + 1] = 0;    // long-record list length (plan_scatter appends)
+    }
 }
 
 __global__ __launch_bounds__(kPlanBlock) void plan_scatter_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, uint64_t count, const uint32_t* __restrict__ blk,
     uint32_t nblocks, Item* __restrict__ items, uint64_t item_cap,
-    uint32_t* __restrict__ full_pos, uint32_t* __restrict__ head_pos)
+    uint32_t* __restrict__ full_pos, uint32_t* __restrict__ head_pos, uint32_t* __restrict__ longs)
 {
     __shared__ uint32_t sh[kPlanBlock / 64];
     const uint64_t r = uint64_t(blockIdx.x) * kPlanBlock + threadIdx.x;
@@ -515,19 +532,15 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter_kernel(
     const uint32_t total_items = blk[4 * nblocks];
     if (total_items > item_cap) return;  // host re-plans with a larger workspace
     const uint32_t rid = uint32_t(r);
-    for (uint32_t j = 0; j < s.nfull; ++j)
-    {
-        // The earliest full chunk also carries init bytes when the head
-        // chunk holds fewer than 4 bytes (or there is none): record start =
-        // chunk start - rem.
-        Item it;
-        it.end = s.e - uint64_t(j) * kChunk;
-        const bool first = j + 1 == s.nfull && s.rem < 4;
-        it.len = kChunk | (first ? s.rem << kItemShiftBit : 0u);
-        it.rec_flag = rid | (first ? kItemStart : 0u);
-        items[pos[0] + j] = it;
-    }
     full_pos[r] = pos[0];
+    if (s.nfull > kLongChunks)
+    {
+        // long record: its full-chunk items are written block-parallel by
+        // long_items_kernel and its chunks combined by long_finalize_kernel
+        longs[atomicAdd(const_cast<uint32_t*>(blk) + 4 * nblocks + 1, 1u)] = rid;
+    }
+    else
+        for (uint32_t j = 0; j < s.nfull; ++j) items[pos[0] + j] = full_item(s, rid, j);
     if (s.hbin)
     {
         const uint32_t hp = s.hbin == 4 ? pos[0] + s.nfull : pos[4 - s.hbin];
@@ -540,6 +553,25 @@ __global__ __launch_bounds__(kPlanBlock) void plan_scatter_kernel(
     }
 }
 
+// Full-chunk items of long records, one workgroup per record.
+__global__ __launch_bounds__(kLongBlock) void long_items_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ counters,
+    const uint32_t* __restrict__ longs, const uint32_t* __restrict__ full_pos,
+    Item* __restrict__ items, uint64_t item_cap)
+{
+    if (counters[0] > item_cap) return;
+    const uint32_t nlong = counters[1];
+    for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x)
+    {
+        const uint32_t r = longs[k];
+        const RecShape s = rec_shape(uint64_t(base) + off[r], len[r]);
+        const uint32_t fp = full_pos[r];
+        for (uint32_t j = threadIdx.x; j < s.nfull; j += kLongBlock)
+            items[fp + j] = full_item(s, r, j);
+    }
+}
+
 hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                            uint64_t count, const VarWorkspace& ws, hipStream_t stream)
 {
@@ -549,7 +581,10 @@ hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint
     hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, 4 * nb);
     hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanBlock), 0, stream,
                        static_cast<const uint8_t*>(base), offsets, lengths, count, ws.blk, nb,
-                       ws.items, ws.item_cap, ws.full_pos, ws.head_pos);
+                       ws.items, ws.item_cap, ws.full_pos, ws.head_pos, ws.longs);
+    hipLaunchKernelGGL(long_items_kernel, dim3(64), dim3(kLongBlock), 0, stream,
+                       static_cast<const uint8_t*>(base), offsets, lengths, ws.blk + 4 * nb,
+                       ws.longs, ws.full_pos, ws.items, ws.item_cap);
     return hipGetLastError();
 }
 
@@ -686,6 +721,8 @@ __global__ __launch_bounds__(256) void crc32c_finalize_kernel(
         c = ~init;
         tail_from = 0;
     }
+    else if (s.nfull > kLongChunks)
+        return;  // long_finalize_kernel
     else
     {
         c = s.hbin ? partial[head_pos[r]] : 0u;
@@ -700,15 +737,92 @@ __global__ __launch_bounds__(256) void crc32c_finalize_kernel(
     out[r] = ~c;
 }
 
+// Long records: raw(main) = Z_{C nfull}(head) ^ XOR_j Z_{C j}(p_j), j counted
+// from the end.  Thread t folds chunks j = t + 1024 k by Horner with
+// Z_{1024 C}, shifts its sum by Z_{C t} (bits of t, tables G^{C 2^b}), and
+// the workgroup XOR-reduces; thread 0 adds the head chunk, the tail bytes
+// and the final inversion.
+__device__ __forceinline__ uint32_t zglob(const uint32_t* g, uint32_t v)
+{
+    return g[v & 0xFFu] ^ g[256 + ((v >> 8) & 0xFFu)] ^ g[512 + ((v >> 16) & 0xFFu)] ^
+           g[768 + (v >> 24)];
+}
+
+__global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits,
+    const uint32_t* __restrict__ counters, const uint32_t* __restrict__ longs,
+    const uint32_t* __restrict__ partial, const uint32_t* __restrict__ full_pos,
+    const uint32_t* __restrict__ head_pos, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint64_t item_cap)
+{
+    __shared__ uint32_t t0[256];
+    __shared__ uint32_t zs[1024];
+    __shared__ uint32_t zc2[10][1024];
+    __shared__ uint32_t red[kLongBlock / 64];
+    if (counters[0] > item_cap) return;
+    const uint32_t nlong = counters[1];
+    if (blockIdx.x >= nlong) return;
+    for (uint32_t i = threadIdx.x; i < 256; i += kLongBlock) t0[i] = tables[kTabT + i];
+    for (uint32_t i = threadIdx.x; i < 1024; i += kLongBlock) zs[i] = tables[kTabZLong + i];
+    for (uint32_t i = threadIdx.x; i < 10 * 1024; i += kLongBlock)
+        zc2[i / 1024][i % 1024] = tables[kTabZC2 + i];
+    __syncthreads();
+    const uint32_t t = threadIdx.x;
+    for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x)
+    {
+        const uint32_t r = longs[k];
+        const uint8_t* p = base + off[r];
+        const uint32_t L = len[r];
+        const RecShape s = rec_shape(uint64_t(p), L);
+        const uint32_t fp = full_pos[r];
+        uint32_t acc = 0;
+        if (t < s.nfull)
+        {
+            const uint32_t n_t = (s.nfull - t + kLongBlock - 1) / kLongBlock;
+            for (uint32_t q = n_t; q-- > 0;)
+                acc = zglob(zs, acc) ^ partial[fp + t + q * kLongBlock];
+            for (int b = 0; b < 10; ++b)
+                if (t & (1u << b)) acc = zglob(zc2[b], acc);
+        }
+        for (int d = 32; d >= 1; d >>= 1) acc ^= __shfl_xor(acc, d);
+        if ((t & 63) == 0) red[t >> 6] = acc;
+        __syncthreads();
+        if (t == 0)
+        {
+            uint32_t c = 0;
+            for (int w = 0; w < kLongBlock / 64; ++w) c ^= red[w];
+            if (s.hbin)
+            {
+                uint32_t h = partial[head_pos[r]];
+                uint64_t n = uint64_t(s.nfull) * kChunk;  // bytes after the head chunk
+                for (int b = 0; n && b < 48; ++b, n >>= 1)
+                    if (n & 1u) h = zglob(pow2 + b * 1024, h);
+                c ^= h;
+            }
+            for (uint64_t i = s.e - uint64_t(p); i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+            out[r] = ~c;
+            (void)inits;  // the init was folded into the first chunk
+        }
+        __syncthreads();
+    }
+}
+
 hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                                const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
-                               uint32_t* out, const uint32_t* tables, hipStream_t stream)
+                               uint32_t* out, const uint32_t* tables, const uint32_t* pow2,
+                               hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
     const uint32_t nb = uint32_t((count + 255) / 256);
     hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(nb), dim3(256), 0, stream,
                        static_cast<const uint8_t*>(base), offsets, lengths, inits, count,
                        ws.partial, ws.full_pos, ws.head_pos, out, tables);
+    const uint32_t grid = uint32_t(count < 256 ? count : 256);
+    hipLaunchKernelGGL(long_finalize_kernel, dim3(grid), dim3(kLongBlock), 0, stream,
+                       static_cast<const uint8_t*>(base), offsets, lengths, inits,
+                       ws.blk + 4 * var_plan_blocks(count), ws.longs, ws.partial, ws.full_pos,
+                       ws.head_pos, out, tables, pow2, ws.item_cap);
     return hipGetLastError();
 }
 

@@ -89,6 +89,11 @@ int init_device(int device)
     make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZ32]), 32);
     make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZ64]), 64);
     make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZChunk]), kChunk);
+    make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZLong]),
+                     uint64_t(kLongBlock) * kChunk);
+    for (int b = 0; b < 10; ++b)
+        make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZC2 + b * 1024]),
+                         uint64_t(kChunk) << b);
     std::vector<uint32_t> pow2(48 * 1024);
     Op32 p = Op32::zero_byte();
     for (int k = 0; k < 64; ++k)
@@ -170,7 +175,7 @@ struct Ctx
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     DevBuf data, off, len, inits, out;  // staging of host batches
-    DevBuf items, partial, full_pos, head_pos, blk;
+    DevBuf items, partial, full_pos, head_pos, blk, longs;
     PinBuf pin_small;                   // plan-size read-back, small host outputs
 
     int open(int ordinal)
@@ -220,7 +225,8 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
     const uint32_t nb = var_plan_blocks(count);
     int st;
     if ((st = c->blk.reserve((4 * size_t(nb) + 4) * 4)) ||
-        (st = c->full_pos.reserve(count * 4)) || (st = c->head_pos.reserve(count * 4)))
+        (st = c->full_pos.reserve(count * 4)) || (st = c->head_pos.reserve(count * 4)) ||
+        (st = c->longs.reserve(count * 4)))
         return st;
     uint64_t cap = total_bytes ? total_bytes / kChunk + 2 * uint64_t(count) + 1
                                : std::max<uint64_t>(c->items.cap / sizeof(Item), 2 * count + 1);
@@ -231,7 +237,8 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
             return st;
         cap = std::min<uint64_t>(c->items.cap / sizeof(Item), c->partial.cap / 4);
         VarWorkspace ws{c->blk.as<uint32_t>(), c->items.as<Item>(), c->partial.as<uint32_t>(),
-                        c->full_pos.as<uint32_t>(), c->head_pos.as<uint32_t>(), cap};
+                        c->full_pos.as<uint32_t>(), c->head_pos.as<uint32_t>(),
+                        c->longs.as<uint32_t>(), cap};
         HIP_TRY(launch_var_plan(base, off, len, count, ws, c->stream));
         if (!total_bytes)
         {
@@ -248,7 +255,8 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
         const uint64_t want_grid = (cap + (kBlock / kTeam) - 1) / (kBlock / kTeam);
         const int grid = int(std::min<uint64_t>(uint64_t(d->cus), std::max<uint64_t>(want_grid, 1)));
         HIP_TRY(launch_var_chunks(inits, count, ws, d->d_tables, grid, c->stream));
-        HIP_TRY(launch_var_finalize(base, off, len, inits, count, ws, out, d->d_tables, c->stream));
+        HIP_TRY(launch_var_finalize(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2,
+                                    c->stream));
         return MI_CRC32C_OK;
     }
     return fail(MI_CRC32C_EHIP, "plan size did not converge");
@@ -652,7 +660,7 @@ int mi_crc32c_pipeline_destroy(mi_crc32c_pipeline* p)
         }
         for (DevBuf* b : {&s.ctx.data, &s.ctx.off, &s.ctx.len, &s.ctx.inits, &s.ctx.out,
                           &s.ctx.items, &s.ctx.partial, &s.ctx.full_pos, &s.ctx.head_pos,
-                          &s.ctx.blk, &s.dseg, &s.dmeta})
+                          &s.ctx.blk, &s.ctx.longs, &s.dseg, &s.dmeta})
             if (b->p) (void)hipFree(b->p);
         for (PinBuf* b : {&s.ctx.pin_small, &s.seg, &s.meta, &s.res})
             if (b->p) (void)hipHostFree(b->p);
