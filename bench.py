@@ -57,6 +57,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="fixed4k", choices=["fixed4k", "zipf", "stream", "pcie4k"],
+                    help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2]; "
+                         "stream = configs[4] (64 MiB host segments, H2D+CRC+D2H); pcie4k = "
+                         "configs[1] bytes starting in pinned host memory")
+    ap.add_argument("--segments", type=int, default=16, help="stream/pcie4k: segments per step")
     ap.add_argument("--records-per-rank", type=int, default=1 << 20)
     ap.add_argument("--record-bytes", type=int, default=RECORD)
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
@@ -150,6 +155,124 @@ def cpu_baseline(args) -> dict:
             "first_crc": int(crc_ref[0])}
 
 
+def run_secondary(args, E) -> dict:
+    """Configs 3 and 5 and the host-inclusive rate of config 2 (one GPU)."""
+    from consus_amd import workload as W
+    gold = golden_digests()
+    res = {"n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u32", "cpu_baseline": None}
+    if args.config == "zipf":
+        R = args.records_per_rank
+        off, ln, total = W.zipf_records(R)
+        data = E.DeviceBuffer(total + 16)
+        data.fill_splitmix64(W.DATA_SEED)
+        d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer(R * 4)
+        d_off.upload(off)
+        d_len.upload(ln)
+        for _ in range(args.warmup):
+            E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
+        E.sync()
+        t0 = time.perf_counter()
+        E.timer_start()
+        for _ in range(args.steps):
+            E.device_batch(data, d_off, d_len, R, out, total_bytes=total, asynchronous=True)
+        ev = E.timer_stop() / args.steps
+        wall = (time.perf_counter() - t0) / args.steps
+        dig = E.crc32c_device(out, R * 4)
+        g = gold.get("zipf_seed0x5eed_data0xda7a5eed_1048576", {})
+        achieved = total / (ev * 1e-3) / 1e9
+        res.update({
+            "metric": "GiB/s CRC32C over device-resident mixed-length records (Zipf 64 B-64 KiB)",
+            "value": round(total / (wall) / 2**30, 2), "unit": "GiB/s",
+            "ms_per_step": round(wall * 1e3, 4),
+            "data": "synthetic: config-3 Zipf lengths, splitmix64 stream 0xDA7A5EED in HBM",
+            "config": {"workload": f"{R} mixed-length records, device-resident, 1 x MI355X "
+                                   f"(BASELINE.json configs[2])", "total_bytes": total},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "step_ms_events": round(ev, 4),
+                         "kernel": "plan + crc32c_chunk_kernel + finalize (whole step)"},
+            "digest_verified": (dig == g.get("digest")) if g and R == 1 << 20 else None,
+            "digests": [f"{dig:#010x}"]})
+        return res
+    # stream / pcie4k: host-resident segments through the H2D -> CRC -> D2H pipeline
+    nseg = args.segments
+    filler = E.DeviceBuffer(W.SEGMENT_BYTES + 64)
+
+    def fill(nbytes, byte_off, seed):
+        # bytes [byte_off, +nbytes) of a stream, produced on the device (8-byte aligned window)
+        a = byte_off & ~7
+        n = nbytes + (byte_off - a)
+        filler.fill_splitmix64(seed, byte_offset=a, nbytes=(n + 7) & ~7)
+        return filler.download(np.uint8, n)[byte_off - a:]
+    segs = []
+    if args.config == "stream":
+        for buf, fo, fl in W.log_segments(nseg, lambda n, o: fill(n, o, W.DATA_SEED)):
+            pb = E.PinnedBuffer(buf.size)
+            pb.array[:] = buf
+            segs.append((pb, fo, fl))
+        metric = "GiB/s host-to-host CRC32C of 64 MiB durable-log segments (H2D+CRC+D2H)"
+        workload = f"{nseg} x 64 MiB durable-log segments in pinned host memory, 1 x MI355X " \
+                   f"(BASELINE.json configs[4])"
+    else:
+        per = W.SEGMENT_BYTES // RECORD
+        for k in range(nseg):
+            pb = E.PinnedBuffer(W.SEGMENT_BYTES)
+            pb.array[:] = fill(W.SEGMENT_BYTES, k * W.SEGMENT_BYTES, SEED)
+            segs.append((pb, np.arange(per, dtype=np.uint64) * RECORD,
+                         np.full(per, RECORD, dtype=np.uint32)))
+        metric = "GiB/s host-to-host CRC32C of 4 KiB records starting in pinned host memory"
+        workload = f"{nseg * per} x 4 KiB records (config-2 bytes) in pinned host memory, " \
+                   f"64 MiB segments, 1 x MI355X"
+    maxrec = max(int(fo.size) for _, fo, _ in segs)
+    pipe = E.Pipeline(W.SEGMENT_BYTES, maxrec, depth=3)
+    outs = [np.zeros(int(fo.size), dtype=np.uint32) for _, fo, _ in segs]
+    total = sum(int(pb.nbytes) for pb, _, _ in segs)
+
+    def step():
+        ts = [pipe.submit(pb, fo, fl, o) for (pb, fo, fl), o in zip(segs, outs)]
+        for t in ts:
+            pipe.wait(t)
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    wall = (time.perf_counter() - t0) / args.steps
+    ok = None
+    if args.config == "stream":
+        g = gold.get("log_segments_64MiB", {}).get("segments", [])
+        dev = E.DeviceBuffer(maxrec * 4)
+        digs = []
+        for o in outs[:len(g)]:
+            dev.upload(o)
+            digs.append(E.crc32c_device(dev, o.size * 4))
+        ok = bool(g) and all(d == x["digest"] for d, x in zip(digs, g))
+    else:
+        dev = E.DeviceBuffer(W.SEGMENT_BYTES // RECORD * 4)
+        digs = []
+        for o in outs:
+            dev.upload(o)
+            digs.append(E.crc32c_device(dev, o.size * 4))
+        from consus_amd.shard import combine_digests
+        whole = combine_digests(digs, [o.size for o in outs])
+        g = gold.get(f"fixed_4096_seed0xc0de_per_1048576", {})
+        ok = (whole == g.get("block_digests", [None])[0]) if nseg * (W.SEGMENT_BYTES // RECORD) \
+            == 1 << 20 else None
+    res.update({"metric": metric, "value": round(total / wall / 2**30, 2), "unit": "GiB/s",
+                "ms_per_step": round(wall * 1e3, 4),
+                "data": "synthetic (SURVEY.md 8(d)); segments pre-built in pinned host memory",
+                "config": {"workload": workload, "segments": nseg, "pipeline_depth": 3,
+                           "bytes_per_step": total},
+                "roofline": {"bound": "pcie", "achieved": round(total / wall / 1e9, 1),
+                             "peak": 63.0, "unit": "GB/s",
+                             "frac": round(total / wall / 1e9 / 63.0, 4), "traffic": None,
+                             "note": "host link PCIe Gen5 x16, 63 GB/s spec"},
+                "digest_verified": ok})
+    pipe.close()
+    return res
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -161,12 +284,19 @@ def main():
 
     # Traffic pass first, before this process touches the GPU.
     traffic, traffic_note = (None, "skipped")
-    if rank == 0 and world == 1 and not args.child_pmc and not args.no_pmc:
+    if rank == 0 and world == 1 and not args.child_pmc and not args.no_pmc and \
+            args.config == "fixed4k":
         traffic, traffic_note = pmc_traffic(args)
 
     # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.
     import consus_amd as E
     E.init(local)
+
+    if args.config != "fixed4k":
+        if world != 1:
+            sys.exit("secondary configs run on one GPU")
+        print(json.dumps(run_secondary(args, E)), flush=True)
+        return
 
     dist = None
     if world > 1:

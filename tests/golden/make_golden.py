@@ -173,6 +173,18 @@ def main() -> None:
         "total_bytes": int(lz.sum(dtype=np.uint64)), "length_digest": orc.digest(lz)[0],
         "digest": dz, "xor": xz, "first16": [int(v) for v in cz[:16]],
     }
+    # cfg 5: 64 MiB durable-log segments (consus_amd/workload.py recipe)
+    from consus_amd.workload import log_segments
+    segs = []
+    for buf, fo, fl in log_segments(4, lambda n, o: orc.fill(n, 0xDA7A5EED, o)):
+        c = ref.batch(buf, fo, fl, threads=THREADS)
+        segs.append({"frames": int(fo.size), "bytes": int(buf.size), "digest": orc.digest(c)[0],
+                     "first_crc": int(c[0])})
+    digests["log_segments_64MiB"] = {
+        "definition": "consus_amd.workload.log_segments: frames [recno BE][len BE][entry][crc] "
+                      "with config-3 entry lengths and stream 0xDA7A5EED entries, greedily packed "
+                      "into 64 MiB segments; digest = crc32c(0, LE CRC vector) per segment",
+        "segments": segs}
     # durable-log framing example (txman/durable_log.cc:54-61, 215-224)
     hdr = (1).to_bytes(8, "big") + (5).to_bytes(8, "big")
     crc = ref.crc32c(ref.crc32c(0, hdr), b"hello")
