@@ -17,6 +17,7 @@ constexpr int kGroupBytes = kRowBytes * kGroupRows;  // 1 KiB
 constexpr int kChunk = 4096;                // variable-length work unit
 constexpr int kBlock = 1024;                // threads per workgroup (16 waves)
 constexpr int kSmallRecord = 32;            // records shorter than this are finished byte-serially
+constexpr uint32_t kFinalizeHead = 1024;    // head chunks up to this size are hashed by finalize
 constexpr uint32_t kLongChunks = 64;        // records with more full chunks take the long path
 constexpr int kLongBlock = 1024;            // threads per long record
 
@@ -28,7 +29,8 @@ constexpr int kTabZ64 = kTabZ32 + 1024;     // G^{64}_j
 constexpr int kTabZChunk = kTabZ64 + 1024;  // G^{4096}_j (chunk combine)
 constexpr int kTabZLong = kTabZChunk + 1024;   // G^{1024*4096} (long-record stride)
 constexpr int kTabZC2 = kTabZLong + 1024;      // G^{4096*2^b}, b = 0..9
-constexpr int kTabZero = kTabZC2 + 10 * 1024;  // 4 zero words (init 0 when inits == nullptr)
+constexpr int kTabP2 = kTabZC2 + 10 * 1024;    // G^{2^k}, k = 0..11 (shifts below 4 KiB)
+constexpr int kTabZero = kTabP2 + 12 * 1024;    // 4 zero words (init 0 when inits == nullptr)
 constexpr int kTabWords = kTabZero + 4;
 
 // LDS image of the record kernels (bytes).

@@ -406,7 +406,9 @@ __device__ __forceinline__ RecShape rec_shape(uint64_t a, uint32_t L)
     const uint64_t m = s.e - a;
     s.nfull = uint32_t(m / kChunk);
     s.rem = uint32_t(m % kChunk);
-    s.hbin = s.rem ? (s.rem + kGroupBytes - 1) / kGroupBytes : 0;
+    // heads of at most kFinalizeHead bytes are not chunk items: the finalize
+    // thread hashes them itself (one team pass + fold would cost more)
+    s.hbin = s.rem > kFinalizeHead ? (s.rem + kGroupBytes - 1) / kGroupBytes : 0;
     return s;
 }
 
@@ -588,114 +590,174 @@ hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint
     return hipGetLastError();
 }
 
-// Fold ~init into the record's first 4 bytes, then zero every byte below the
-// chunk start.  `o` = byte offset of this lane's 16 B from the chunk start,
-// `shift` = chunk start - record start (0..3).
-__device__ __forceinline__ uint4 head_fix(uint4 d, int32_t o, bool start, uint32_t xinit,
-                                          int32_t shift)
+// Zero every byte below the chunk start, branch-free; `o` = byte offset of
+// this lane's 16 B from the chunk start (rows with o <= -16 become zero).
+__device__ __forceinline__ uint4 mask_below_start(uint4 d, int32_t o)
 {
     uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
     {
-        const int32_t rel = o + shift + 4 * q;  // from the record start
-        if (start && rel > -4 && rel < 4)
-            w[q] ^= rel >= 0 ? (xinit >> (8 * rel)) : (xinit << (8 * -rel));
-        const int32_t oc = o + 4 * q;  // from the chunk start
-        if (oc <= -4)
-            w[q] = 0;
-        else if (oc < 0)
-            w[q] &= 0xFFFFFFFFu << (8 * -oc);
+        const int32_t below = -(o + 4 * q);  // bytes of this dword below the start
+        const uint32_t keep = below <= 0 ? 0xFFFFFFFFu
+                                         : (below >= 4 ? 0u : (0xFFFFFFFFu << (8 * below)));
+        w[q] &= keep;
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
-    const Item* __restrict__ items, const uint32_t* __restrict__ total_items,
-    const uint32_t* __restrict__ inits, uint32_t* __restrict__ partial, uint64_t item_cap,
-    const uint32_t* __restrict__ tables)
+// One chunk as a team sees it: row 0 of group 0 of this lane starts at p0,
+// o0 bytes from the chunk start (negative = before it; such rows load from
+// `clamp`, a valid address in the chunk's first 16-byte block, and are
+// zeroed by head_fix).
+struct ChunkView
 {
-    stage_tables(tables);
-    const uint32_t n_items = *total_items;
-    if (n_items > item_cap) return;
+    const uint8_t* p0;
+    int32_t coff;  // clamp address - p0
+    int32_t o0;
+};
 
-    const uint32_t tl = threadIdx.x & (kTeam - 1);
-    const uint32_t li = lane_info();
+template <int G>
+__device__ __forceinline__ ChunkView view_of(const Item& it, uint32_t tl)
+{
+    ChunkView v;
+    const uint32_t len = it.len & kItemLenMask;
+    v.o0 = int32_t(len) - G * kGroupBytes + int32_t(tl) * 16;
+    v.p0 = reinterpret_cast<const uint8_t*>(it.end) - G * kGroupBytes + tl * 16;
+    // first 16-byte block of the chunk, relative to p0
+    v.coff = -v.o0 - int32_t((it.end - len) & 15u);
+    return v;
+}
+
+// Items [lo, hi) all have G groups (the plan bins them).  Same discipline as
+// crc32c_fixed_pipe_kernel: every group's 8 loads are unconditional and
+// issued (sched_barrier) while the previous group is folded; item
+// descriptors run two items ahead, so the loop-carried loads are identical
+// on every path and vmcnt stays exact.  The init is not applied here (the
+// finalize kernels add Z_L(~init)); only head chunks, whose start is not on
+// the row grid, need masking, under a wave-uniform branch per group.  For
+// odd G two items are unrolled per iteration so the A/B buffers alternate.
+template <int G>
+__device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32_t lo, uint32_t hi,
+                                          uint32_t* __restrict__ partial, uint32_t team,
+                                          uint32_t team0, uint32_t nteams, uint32_t tl,
+                                          uint32_t li)
+{
+    if (hi <= lo || lo + team0 >= hi) return;
+    constexpr int U = (G % 2 == 0) ? 1 : 2;  // items per loop iteration
+    const uint32_t iters_items = (hi - lo - team0 + nteams - 1) / nteams;
+    const uint32_t iters = (iters_items + U - 1) / U;
+    auto idx_of = [&](uint32_t k) {
+        const uint32_t i = lo + team + k * nteams;
+        return i < hi ? i : hi - 1;
+    };
+    auto load_group = [&](uint4 (&buf)[kGroupRows], const ChunkView& v, int g) {
+#pragma unroll
+        for (int r = 0; r < kGroupRows; ++r)
+        {
+            const int32_t o = v.o0 + g * kGroupBytes + r * kRowBytes;
+            buf[r] = load16(v.p0 + (o > -16 ? g * kGroupBytes + r * kRowBytes : v.coff));
+        }
+    };
+
+    uint4 A[kGroupRows], B[kGroupRows];
+    Item nit = items[idx_of(1)];  // descriptors run two items ahead of the data
+    ChunkView cur = view_of<G>(items[idx_of(0)], tl);
+    load_group(A, cur, 0);
+    uint32_t k = 0;
+    for (uint32_t iter = 0; iter < iters; ++iter)
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u, ++k)
+        {
+            const Item nnit = items[idx_of(k + 2)];
+            ChunkView nxt = cur;
+            uint32_t V[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+            {
+                const int parity = (u * G + g) % 2;  // buffer holding group g
+                uint4(&bc)[kGroupRows] = parity == 0 ? A : B;
+                uint4(&bn)[kGroupRows] = parity == 0 ? B : A;
+                if (g + 1 < G)
+                    load_group(bn, cur, g + 1);
+                else
+                {
+                    nxt = view_of<G>(nit, tl);
+                    load_group(bn, nxt, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const int32_t og = cur.o0 + g * kGroupBytes;  // row 0 of this group
+                if (__builtin_amdgcn_ballot_w64(og < 0))     // some team starts in this group
+                {
+#pragma unroll
+                    for (int r = 0; r < kGroupRows; ++r)
+                        row_update(V, mask_below_start(bc[r], og + r * kRowBytes), li);
+                }
+                else
+                {
+#pragma unroll
+                    for (int r = 0; r < kGroupRows; ++r) row_update(V, bc[r], li);
+                }
+            }
+            const uint32_t raw = team_fold(V);
+            const uint32_t i = lo + team + k * nteams;
+            if (tl == 0 && i < hi) partial[i] = raw;
+            cur = nxt;
+            nit = nnit;
+        }
+    }
+}
+
+// One launch per bin (G = 4, 3, 2, 1): each specialisation alone fits the
+// 128-VGPR budget of a 16-wave workgroup; inlined together they spill.
+template <int G>
+__global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
+    const Item* __restrict__ items, const uint32_t* __restrict__ blk, uint32_t nblocks,
+    uint32_t* __restrict__ partial, uint64_t item_cap, const uint32_t* __restrict__ tables)
+{
+    const uint32_t n_items = blk[4 * nblocks];
+    if (n_items > item_cap) return;
+    // bin b (0..3 = 4, 3, 2, 1 groups) is [blk[b * nblocks], blk[(b + 1) * nblocks])
+    const uint32_t b = 4 - G;
+    const uint32_t lo = blk[b * nblocks];
+    const uint32_t hi = b == 3 ? n_items : blk[(b + 1) * nblocks];
     const uint32_t team = (blockIdx.x * kBlock + threadIdx.x) / kTeam;
     const uint32_t nteams = gridDim.x * kBlock / kTeam;
-    const uint32_t team0 = team & ~7u;
-
-    for (uint32_t w0 = team0; w0 < n_items; w0 += nteams)
-    {
-        const uint32_t idx = w0 + (team - team0);
-        const bool valid = idx < n_items;
-        Item it{16, 0, 0};
-        if (valid) it = items[idx];
-        const int32_t shift = int32_t(it.len >> kItemShiftBit);
-        it.len &= kItemLenMask;
-        const uint32_t gt = (it.len + kGroupBytes - 1) / kGroupBytes;
-        // wave-uniform group count = max over the 8 teams
-        uint32_t gw = gt;
-        gw = max(gw, uint32_t(__shfl_xor(int(gw), 8)));
-        gw = max(gw, uint32_t(__shfl_xor(int(gw), 16)));
-        gw = max(gw, uint32_t(__shfl_xor(int(gw), 32)));
-        const bool start = (it.rec_flag & kItemStart) != 0;
-        const uint32_t xinit =
-            start ? (inits ? ~inits[it.rec_flag & ~kItemStart] : 0xFFFFFFFFu) : 0u;
-        // offset of this lane's column in row 0 of group 0, relative to chunk start
-        const int32_t o0 = int32_t(it.len) - int32_t(gw * kGroupBytes) + int32_t(tl) * 16;
-        const uint8_t* p0 = reinterpret_cast<const uint8_t*>(it.end) - int64_t(gw) * kGroupBytes +
-                            int64_t(tl) * 16;
-
-        uint32_t V[4] = {0, 0, 0, 0};
-        uint4 A[kGroupRows], B[kGroupRows];
-        auto issue = [&](uint4 (&buf)[kGroupRows], uint32_t g) {
-#pragma unroll
-            for (int r = 0; r < kGroupRows; ++r)
-            {
-                const int32_t o = o0 + int32_t(g) * kGroupBytes + r * kRowBytes;
-                buf[r] = (valid && o > -16)
-                             ? load16(p0 + int64_t(g) * kGroupBytes + r * kRowBytes)
-                             : make_uint4(0, 0, 0, 0);
-            }
-        };
-        auto process = [&](uint4 (&buf)[kGroupRows], uint32_t g) {
-#pragma unroll
-            for (int r = 0; r < kGroupRows; ++r)
-            {
-                const int32_t o = o0 + int32_t(g) * kGroupBytes + r * kRowBytes;
-                uint4 d = buf[r];
-                if (__builtin_expect(o > -20 && o < 4, 0)) d = head_fix(d, o, start, xinit, shift);
-                row_update(V, d, li);
-            }
-        };
-        issue(A, 0);
-        if (gw > 1) issue(B, 1);
-        for (uint32_t g = 0; g < gw; g += 2)
-        {
-            process(A, g);
-            if (g + 2 < gw) issue(A, g + 2);
-            if (g + 1 < gw)
-            {
-                process(B, g + 1);
-                if (g + 3 < gw) issue(B, g + 3);
-            }
-        }
-        const uint32_t raw = team_fold(V);
-        if (valid && tl == 0) partial[idx] = raw;
-    }
+    if (hi <= lo || lo + (blockIdx.x * kBlock) / kTeam >= hi) return;  // whole workgroup idle
+    stage_tables(tables);
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    chunk_bin<G>(items, lo, hi, partial, team, team & ~7u, nteams, tl, lane_info());
 }
 
 hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
                              const uint32_t* tables, int grid, hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
-    const uint32_t* total = ws.blk + 4 * var_plan_blocks(count);
-    hipLaunchKernelGGL(crc32c_chunk_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream, ws.items,
-                       total, inits, ws.partial, ws.item_cap, tables);
+    const uint32_t nb = var_plan_blocks(count);
+    (void)inits;  // applied by the finalize kernels
+#define MI_LAUNCH_CHUNK(GG)                                                                      \
+    hipLaunchKernelGGL(crc32c_chunk_kernel<GG>, dim3(grid), dim3(kBlock), kLdsBytes, stream,    \
+                       ws.items, ws.blk, nb, ws.partial, ws.item_cap, tables)
+    MI_LAUNCH_CHUNK(4);
+    MI_LAUNCH_CHUNK(3);
+    MI_LAUNCH_CHUNK(2);  // bin 1 (heads <= 1 KiB) is hashed by the finalize kernel
+#undef MI_LAUNCH_CHUNK
     return hipGetLastError();
 }
 
+// Z_n(v) through a G^n table set (LDS or global).
+__device__ __forceinline__ uint32_t zglob(const uint32_t* g, uint32_t v)
+{
+    return g[v & 0xFFu] ^ g[256 + ((v >> 8) & 0xFFu)] ^ g[512 + ((v >> 16) & 0xFFu)] ^
+           g[768 + (v >> 24)];
+}
+
+// One thread per record: short records byte-serially; otherwise the
+// register after the head chunk when started from ~init -- hashed here for
+// heads <= kFinalizeHead (slice-by-16 over aligned 16-B loads), or
+// Z_rem(~init) ^ raw(head) from the chunk kernel (identity 1) -- carried over
+// the full chunks by Horner with Z_4096, then the < 16-byte tail.
 __global__ __launch_bounds__(256) void crc32c_finalize_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
@@ -703,37 +765,52 @@ __global__ __launch_bounds__(256) void crc32c_finalize_kernel(
     const uint32_t* __restrict__ head_pos, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables)
 {
-    __shared__ uint32_t t0[256];
+    __shared__ uint32_t T[16][256];
     __shared__ uint32_t zc[1024];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) t0[i] = tables[kTabT + i];
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) T[i / 256][i % 256] = tables[kTabT + i];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) zc[i] = tables[kTabZChunk + i];
     __syncthreads();
     const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (r >= count) return;
     const uint8_t* p = base + off[r];
     const uint32_t L = len[r];
-    const uint32_t init = inits ? inits[r] : 0u;
+    const uint32_t x = ~(inits ? inits[r] : 0u);
     const RecShape s = rec_shape(uint64_t(p), L);
-    uint32_t c;
-    uint64_t tail_from;
-    if (L < uint32_t(kSmallRecord))
+    uint32_t c = x;
+    uint64_t tail_from = 0;
+    if (L >= uint32_t(kSmallRecord))
     {
-        c = ~init;
-        tail_from = 0;
-    }
-    else if (s.nfull > kLongChunks)
-        return;  // long_finalize_kernel
-    else
-    {
-        c = s.hbin ? partial[head_pos[r]] : 0u;
+        if (s.nfull > kLongChunks) return;  // long_finalize_kernel
+        if (s.hbin)
+        {
+            const uint32_t* p2 = tables + kTabP2;  // L2-resident G^{2^b}
+            for (int b = 0; b < 12; ++b)
+                if (s.rem & (1u << b)) c = zglob(p2 + b * 1024, c);
+            c ^= partial[head_pos[r]];
+        }
+        else if (s.rem)
+        {
+            // head [p, p + rem): bytes up to 16-byte alignment, then slice-by-16
+            const uint8_t* q = p;
+            const uint8_t* hend = p + s.rem;  // 16-aligned
+            while ((uintptr_t(q) & 15u) && q < hend) c = T[0][(c ^ *q++) & 0xFFu] ^ (c >> 8);
+            for (; q < hend; q += 16)
+            {
+                const uint4 w = *reinterpret_cast<const uint4*>(q);
+                const uint32_t a = c ^ w.x;
+                c = T[15][a & 0xFFu] ^ T[14][(a >> 8) & 0xFFu] ^ T[13][(a >> 16) & 0xFFu] ^
+                    T[12][a >> 24] ^ T[11][w.y & 0xFFu] ^ T[10][(w.y >> 8) & 0xFFu] ^
+                    T[9][(w.y >> 16) & 0xFFu] ^ T[8][w.y >> 24] ^ T[7][w.z & 0xFFu] ^
+                    T[6][(w.z >> 8) & 0xFFu] ^ T[5][(w.z >> 16) & 0xFFu] ^ T[4][w.z >> 24] ^
+                    T[3][w.w & 0xFFu] ^ T[2][(w.w >> 8) & 0xFFu] ^ T[1][(w.w >> 16) & 0xFFu] ^
+                    T[0][w.w >> 24];
+            }
+        }
         const uint32_t fp = full_pos[r];
-        for (uint32_t j = s.nfull; j-- > 0;)
-            c = (zc[c & 0xFFu] ^ zc[256 + ((c >> 8) & 0xFFu)] ^ zc[512 + ((c >> 16) & 0xFFu)] ^
-                 zc[768 + (c >> 24)]) ^
-                partial[fp + j];
+        for (uint32_t j = s.nfull; j-- > 0;) c = zglob(zc, c) ^ partial[fp + j];
         tail_from = s.e - uint64_t(p);
     }
-    for (uint64_t i = tail_from; i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+    for (uint64_t i = tail_from; i < L; ++i) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
     out[r] = ~c;
 }
 
@@ -742,12 +819,6 @@ __global__ __launch_bounds__(256) void crc32c_finalize_kernel(
 // Z_{1024 C}, shifts its sum by Z_{C t} (bits of t, tables G^{C 2^b}), and
 // the workgroup XOR-reduces; thread 0 adds the head chunk, the tail bytes
 // and the final inversion.
-__device__ __forceinline__ uint32_t zglob(const uint32_t* g, uint32_t v)
-{
-    return g[v & 0xFFu] ^ g[256 + ((v >> 8) & 0xFFu)] ^ g[512 + ((v >> 16) & 0xFFu)] ^
-           g[768 + (v >> 24)];
-}
-
 __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits,
@@ -792,17 +863,23 @@ __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
         {
             uint32_t c = 0;
             for (int w = 0; w < kLongBlock / 64; ++w) c ^= red[w];
+            // register after the head chunk when started from ~init (see the
+            // finalize kernel), carried over the full chunks by Z_{C nfull}
+            uint32_t h = ~(inits ? inits[r] : 0u);
             if (s.hbin)
             {
-                uint32_t h = partial[head_pos[r]];
-                uint64_t n = uint64_t(s.nfull) * kChunk;  // bytes after the head chunk
-                for (int b = 0; n && b < 48; ++b, n >>= 1)
-                    if (n & 1u) h = zglob(pow2 + b * 1024, h);
-                c ^= h;
+                for (int b = 0; b < 12; ++b)
+                    if (s.rem & (1u << b)) h = zglob(pow2 + b * 1024, h);
+                h ^= partial[head_pos[r]];
             }
+            else
+                for (uint32_t i = 0; i < s.rem; ++i) h = t0[(h ^ p[i]) & 0xFFu] ^ (h >> 8);
+            uint64_t n = uint64_t(s.nfull) * kChunk;  // bytes after the head chunk
+            for (int b = 0; n && b < 48; ++b, n >>= 1)
+                if (n & 1u) h = zglob(pow2 + b * 1024, h);
+            c ^= h;
             for (uint64_t i = s.e - uint64_t(p); i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
             out[r] = ~c;
-            (void)inits;  // the init was folded into the first chunk
         }
         __syncthreads();
     }
@@ -898,9 +975,12 @@ hipError_t configure_kernels()
     for (const void* f : k)
         if (e == hipSuccess)
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_chunk_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    const void* c[] = {reinterpret_cast<const void*>(&crc32c_chunk_kernel<4>),
+                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<3>),
+                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<2>)};
+    for (const void* f : c)
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     return e;
 }
 

@@ -94,6 +94,9 @@ int init_device(int device)
     for (int b = 0; b < 10; ++b)
         make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZC2 + b * 1024]),
                          uint64_t(kChunk) << b);
+    for (int b = 0; b < 12; ++b)
+        make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabP2 + b * 1024]),
+                         uint64_t(1) << b);
     std::vector<uint32_t> pow2(48 * 1024);
     Op32 p = Op32::zero_byte();
     for (int k = 0; k < 64; ++k)

@@ -45,8 +45,10 @@ __global__ __launch_bounds__(256) void probe_stream(const uint4* __restrict__ p,
 // 4 KiB, 16 loads per lane per step, persistent grid of 1024-thread blocks.
 template <bool NT>
 __global__ __launch_bounds__(1024, 1) void probe_team(const uint8_t* __restrict__ base,
-                                                      uint64_t count, uint32_t* __restrict__ sink)
+                                                      uint64_t count, uint32_t* __restrict__ sink,
+                                                      uint32_t skew = 0)
 {
+    base += skew;
     const uint32_t tl = threadIdx.x & 7u;
     const uint64_t team = (uint64_t(blockIdx.x) * 1024 + threadIdx.x) / 8;
     const uint64_t nteams = uint64_t(gridDim.x) * 1024 / 8;
@@ -83,8 +85,11 @@ extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid,
             case 0: hipLaunchKernelGGL((probe_stream<false, 8>), dim3(grid), dim3(256), 0, 0, p, n16, sink); break;
             case 1: hipLaunchKernelGGL((probe_stream<true, 8>), dim3(grid), dim3(256), 0, 0, p, n16, sink); break;
             case 2: hipLaunchKernelGGL((probe_stream<false, 16>), dim3(grid), dim3(256), 0, 0, p, n16, sink); break;
-            case 3: hipLaunchKernelGGL((probe_team<false>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
-            case 4: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+            case 3: hipLaunchKernelGGL((probe_team<false>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink, 0u); break;
+            case 4: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink, 0u); break;
+            case 5: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096 - 1, sink, 16u); break;
+            case 6: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096 - 1, sink, 64u); break;
+            case 7: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096 - 1, sink, 80u); break;
         }
     };
     launch();
