@@ -17,8 +17,9 @@ constexpr int kGroupBytes = kRowBytes * kGroupRows;  // 1 KiB
 constexpr int kChunk = 4096;                // variable-length work unit
 constexpr int kBlock = 1024;                // threads per workgroup (16 waves)
 constexpr int kSmallRecord = 32;            // records shorter than this are finished byte-serially
-constexpr uint32_t kFinalizeHead = 1024;    // head chunks up to this size are hashed by finalize
-constexpr uint32_t kLongChunks = 64;        // records with more full chunks take the long path
+constexpr uint32_t kLongChunks = 64;        // records with more interior chunks take the long path
+// Plan bins: 0, 1, 2 = pieces of 4, 3, 2 groups; 3 + (8 - R) = one group of R rows (R = 8..1)
+constexpr uint32_t kBins = 11;
 constexpr int kLongBlock = 1024;            // threads per long record
 
 // Global table image uploaded once per device (u32 words).
@@ -29,8 +30,9 @@ constexpr int kTabZ64 = kTabZ32 + 1024;     // G^{64}_j
 constexpr int kTabZChunk = kTabZ64 + 1024;  // G^{4096}_j (chunk combine)
 constexpr int kTabZLong = kTabZChunk + 1024;   // G^{1024*4096} (long-record stride)
 constexpr int kTabZC2 = kTabZLong + 1024;      // G^{4096*2^b}, b = 0..9
-constexpr int kTabP2 = kTabZC2 + 10 * 1024;    // G^{2^k}, k = 0..11 (shifts below 4 KiB)
-constexpr int kTabZero = kTabP2 + 12 * 1024;    // 4 zero words (init 0 when inits == nullptr)
+constexpr int kTabP2 = kTabZC2 + 10 * 1024;    // G^{2^k}, k = 0..12 (shifts up to 4 KiB)
+constexpr int kTabZInv128 = kTabP2 + 13 * 1024; // Z_{-128} = (Z_128)^{-1}
+constexpr int kTabZero = kTabZInv128 + 1024;    // 4 zero words (init 0 when inits == nullptr)
 constexpr int kTabWords = kTabZero + 4;
 
 // LDS image of the record kernels (bytes).
@@ -40,18 +42,17 @@ constexpr uint32_t kLdsZ32 = kLdsT + 16384;
 constexpr uint32_t kLdsZ64 = kLdsZ32 + 4096;
 constexpr uint32_t kLdsBytes = kLdsZ64 + 4096;  // 155648
 
-// One unit of variable-length work: the bytes [end - len, end) of a record,
-// end 16-byte aligned.  rec_flag = record index | kItemStart if the chunk
-// holds any of the record's first 4 bytes (the init is folded in there).
+// One unit of variable-length work ("piece"): the part of a record inside one
+// 4 KiB-aligned chunk of the address space.  A team hashes the 128-B-aligned
+// window [wend - G KiB, wend), wend = the piece end rounded up to 128, with
+// the bytes before the piece start and the m bytes after its end masked.
 struct Item
 {
-    uint64_t end;
-    uint32_t len;
-    uint32_t rec_flag;
+    uint64_t wend;
+    uint32_t lenw_m;  // (wend - piece start) | m << kItemMShift
+    uint32_t rec;
 };
-constexpr uint32_t kItemStart = 0x80000000u;
-// Item::len = bytes (<= kChunk) | (chunk start - record start) << kItemShiftBit
-constexpr uint32_t kItemShiftBit = 16;
+constexpr uint32_t kItemMShift = 16;
 constexpr uint32_t kItemLenMask = 0xFFFFu;
 
 hipError_t configure_kernels();
@@ -63,11 +64,12 @@ hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const u
 // Variable-length pipeline.  `ws_*` are engine-owned device workspaces.
 struct VarWorkspace
 {
-    uint32_t* blk;        // 4 * nblocks + 4 u32 (bin counts -> offsets, then totals)
+    uint32_t* blk;        // kBins * nblocks + 4 u32 (bin counts -> offsets, then totals)
     Item* items;          // capacity `item_cap`
     uint32_t* partial;    // capacity `item_cap`
-    uint32_t* full_pos;   // count
-    uint32_t* head_pos;   // count
+    uint32_t* first_pos;  // count: item of the record's first piece
+    uint32_t* int_pos;    // count: first interior (full 4 KiB) piece
+    uint32_t* last_pos;   // count: item of the last piece (records with >= 2 pieces)
     uint32_t* longs;      // count (records on the long path)
     uint64_t item_cap;
 };

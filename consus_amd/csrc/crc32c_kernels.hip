@@ -373,15 +373,17 @@ hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const u
 }
 
 // ---------------------------------------------------------------------------
-// Variable-length batches: plan -> chunks -> finalize.
-//   plan:     each record's 16-aligned main part [a, e) is cut into 4 KiB
-//             chunks aligned backward from e plus one head chunk of the
-//             remainder; chunks are bucketed by their 1-KiB group count
-//             (4 first) so the 8 teams of a wave get equal work.
-//   chunks:   one team per chunk -> raw CRC of the chunk (partial[item]).
-//   finalize: one thread per record: Horner over its chunks with Z_4096,
-//             then the <16-byte tail byte-serially; short records entirely
-//             byte-serially.
+// Variable-length batches: plan -> pieces -> finalize.
+//   plan:     a record [a, E) is cut at the multiples of 4 KiB of the address
+//             space into n pieces (first, n-2 interior full chunks, last);
+//             pieces are bucketed by their 1-KiB group count (4 first) so the
+//             8 teams of a wave get equal work.  Every team window is 128-B
+//             aligned in memory (a 16-B skew of the rows costs 16 % of HBM
+//             bandwidth, tools/probe.py).
+//   pieces:   one team per piece -> R = raw(window) = Z_m(raw(piece)).
+//   finalize: one thread per record: Horner from ~init over its pieces,
+//             undoing the last piece's m trailing zeros with
+//             Z_{-m} = Z_{-128} o Z_{128-m}; records < 32 B byte-serially.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPlanBlock = 256;
 
@@ -392,40 +394,65 @@ uint32_t var_plan_blocks(uint64_t count)
 
 struct RecShape
 {
-    uint64_t e;      // 16-aligned end of the main part
-    uint32_t nfull;  // full 4 KiB chunks
-    uint32_t rem;    // bytes in the head chunk (0 = none)
-    uint32_t hbin;   // 1..4 groups of the head chunk, 0 = none
+    uint64_t a, E;  // record bytes [a, E) (absolute addresses)
+    uint64_t k0;    // chunk index of the first piece
+    uint32_t n;     // pieces; 0 = short record (finalize hashes it byte-serially)
 };
 
 __device__ __forceinline__ RecShape rec_shape(uint64_t a, uint32_t L)
 {
-    RecShape s{0, 0, 0, 0};
-    if (L < uint32_t(kSmallRecord)) return s;
-    s.e = (a + L) & ~uint64_t(15);
-    const uint64_t m = s.e - a;
-    s.nfull = uint32_t(m / kChunk);
-    s.rem = uint32_t(m % kChunk);
-    // heads of at most kFinalizeHead bytes are not chunk items: the finalize
-    // thread hashes them itself (one team pass + fold would cost more)
-    s.hbin = s.rem > kFinalizeHead ? (s.rem + kGroupBytes - 1) / kGroupBytes : 0;
+    RecShape s{a, a + L, a / kChunk, 0};
+    if (L >= uint32_t(kSmallRecord)) s.n = uint32_t((s.E - 1) / kChunk - s.k0 + 1);
     return s;
 }
 
-__device__ __forceinline__ Item full_item(const RecShape& s, uint32_t rid, uint32_t j)
+__device__ __forceinline__ uint64_t piece_start(const RecShape& s, uint32_t i)
 {
-    // The earliest full chunk also carries init bytes when the head chunk
-    // holds fewer than 4 bytes (or there is none): record start = chunk
-    // start - rem.
+    const uint64_t c = (s.k0 + i) * kChunk;
+    return c > s.a ? c : s.a;
+}
+
+__device__ __forceinline__ uint64_t piece_end(const RecShape& s, uint32_t i)
+{
+    const uint64_t c = (s.k0 + i + 1) * kChunk;
+    return c < s.E ? c : s.E;
+}
+
+__device__ __forceinline__ Item piece_item(const RecShape& s, uint32_t i, uint32_t rec)
+{
+    const uint64_t ps = piece_start(s, i), pe = piece_end(s, i);
+    const uint64_t w = (pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
     Item it;
-    it.end = s.e - uint64_t(j) * kChunk;
-    const bool first = j + 1 == s.nfull && s.rem < 4;
-    it.len = kChunk | (first ? s.rem << kItemShiftBit : 0u);
-    it.rec_flag = rid | (first ? kItemStart : 0u);
+    it.wend = w;
+    it.lenw_m = uint32_t(w - ps) | (uint32_t(w - pe) << kItemMShift);
+    it.rec = rec;
     return it;
 }
 
-// Block-wide exclusive scan of one u32 per thread (256 threads, 4 waves).
+// bins 0, 1, 2 = 4, 3, 2 groups of 8 rows; 3 + (8 - R) = one group, R rows
+__device__ __forceinline__ uint32_t piece_bin(const RecShape& s, uint32_t i)
+{
+    const uint64_t ps = piece_start(s, i), pe = piece_end(s, i);
+    const uint64_t w = (pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
+    const uint32_t rows = uint32_t((w - (ps & ~uint64_t(kRowBytes - 1))) / kRowBytes);
+    return rows > kGroupRows ? 4 - (rows + kGroupRows - 1) / kGroupRows : 3 + (kGroupRows - rows);
+}
+
+// items per bin for one record: first, interior (bin 0), last
+__device__ __forceinline__ void rec_counts(const RecShape& s, uint32_t c[kBins])
+{
+#pragma unroll
+    for (uint32_t b = 0; b < kBins; ++b) c[b] = 0;
+    if (s.n == 0) return;
+    c[piece_bin(s, 0)] += 1;
+    if (s.n >= 2)
+    {
+        c[0] += s.n - 2;
+        c[piece_bin(s, s.n - 1)] += 1;
+    }
+}
+
+// Block-wide exclusive scan of one u32 per thread (kPlanBlock threads).
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t& total)
 {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -455,15 +482,10 @@ __global__ __launch_bounds__(kPlanBlock) void plan_count_kernel(
 {
     __shared__ uint32_t sh[kPlanBlock / 64];
     const uint64_t r = uint64_t(blockIdx.x) * kPlanBlock + threadIdx.x;
-    RecShape s{0, 0, 0, 0};
-    if (r < count) s = rec_shape(uint64_t(base) + off[r], len[r]);
-    uint32_t c[4];
-    c[0] = s.nfull + (s.hbin == 4);  // bin order: 4, 3, 2, 1 groups
-    c[1] = s.hbin == 3;
-    c[2] = s.hbin == 2;
-    c[3] = s.hbin == 1;
+    uint32_t c[kBins] = {};
+    if (r < count) rec_counts(rec_shape(uint64_t(base) + off[r], len[r]), c);
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (uint32_t b = 0; b < kBins; ++b)
     {
         uint32_t total;
         block_exscan(c[b], sh, total);
@@ -471,20 +493,37 @@ __global__ __launch_bounds__(kPlanBlock) void plan_count_kernel(
     }
 }
 
-// Single-workgroup exclusive scan over n u32 (in place); writes the grand
-// total to blk[n].  n = 4 * nblocks is small (16K for 1M records).
+// Single-workgroup exclusive scan over n u32 (in place), in LDS tiles of
+// 16K entries loaded and stored coalesced; each thread scans 16 consecutive
+// entries of the tile (index padded by one word per 32 against bank
+// conflicts).  Writes the grand total to blk[n] and zeroes the long-record
+// counter blk[n + 1].
+constexpr uint32_t kScanPer = 16;
+constexpr uint32_t kScanTile = 1024 * kScanPer;
+
+__device__ __forceinline__ uint32_t scan_slot(uint32_t i) { return i + (i >> 5); }
+
 __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ blk, uint32_t n)
 {
+    __shared__ uint32_t tile[kScanTile + kScanTile / 32];
     __shared__ uint32_t sh[16];
     __shared__ uint32_t carry;
     if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    for (uint32_t base = 0; base < n; base += 1024)
+    for (uint32_t base = 0; base < n; base += kScanTile)
     {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < n ? blk[i] : 0;
-        uint32_t x = v;
+        const uint32_t cnt = min(kScanTile, n - base);
+        for (uint32_t i = threadIdx.x; i < kScanTile; i += 1024)
+            tile[scan_slot(i)] = i < cnt ? blk[base + i] : 0u;
+        __syncthreads();
+        uint32_t v[kScanPer], sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kScanPer; ++j)
+        {
+            v[j] = tile[scan_slot(threadIdx.x * kScanPer + j)];
+            sum += v[j];
+        }
+        uint32_t x = sum;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1)
         {
@@ -493,73 +532,82 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
         }
         if (lane == 63) sh[wave] = x;
         __syncthreads();
-        uint32_t woff = 0, tot = 0;
+        uint32_t run = carry + x - sum, tot = 0;
         for (uint32_t w = 0; w < 16; ++w)
         {
-            if (w < wave) woff += sh[w];
+            if (w < wave) run += sh[w];
             tot += sh[w];
         }
-        const uint32_t c = carry;
-        if (i < n) blk[i] = c + woff + x - v;
+#pragma unroll
+        for (uint32_t j = 0; j < kScanPer; ++j)
+        {
+            tile[scan_slot(threadIdx.x * kScanPer + j)] = run;
+            run += v[j];
+        }
         __syncthreads();
-        if (threadIdx.x == 0) carry = c + tot;
+        for (uint32_t i = threadIdx.x; i < cnt; i += 1024) blk[base + i] = tile[scan_slot(i)];
+        if (threadIdx.x == 0) carry += tot;
         __syncthreads();
     }
     if (threadIdx.x == 0)
     {
-        blk[n] = carry;    // total items
-        blk[n + 1] = 0;    // long-record list length (plan_scatter appends)
+        blk[n] = carry;  // total items
+        blk[n + 1] = 0;  // long-record list length (plan_scatter appends)
     }
 }
 
 __global__ __launch_bounds__(kPlanBlock) void plan_scatter_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, uint64_t count, const uint32_t* __restrict__ blk,
+    const uint32_t* __restrict__ len, uint64_t count, uint32_t* __restrict__ blk,
     uint32_t nblocks, Item* __restrict__ items, uint64_t item_cap,
-    uint32_t* __restrict__ full_pos, uint32_t* __restrict__ head_pos, uint32_t* __restrict__ longs)
+    uint32_t* __restrict__ first_pos, uint32_t* __restrict__ int_pos,
+    uint32_t* __restrict__ last_pos, uint32_t* __restrict__ longs)
 {
     __shared__ uint32_t sh[kPlanBlock / 64];
     const uint64_t r = uint64_t(blockIdx.x) * kPlanBlock + threadIdx.x;
     RecShape s{0, 0, 0, 0};
-    if (r < count) s = rec_shape(uint64_t(base) + off[r], len[r]);
-    uint32_t c[4] = {s.nfull + (s.hbin == 4), s.hbin == 3, s.hbin == 2, s.hbin == 1};
-    uint32_t pos[4];
+    uint32_t c[kBins] = {};
+    if (r < count)
+    {
+        s = rec_shape(uint64_t(base) + off[r], len[r]);
+        rec_counts(s, c);
+    }
+    uint32_t pos[kBins];
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (uint32_t b = 0; b < kBins; ++b)
     {
         uint32_t total;
         pos[b] = blk[b * nblocks + blockIdx.x] + block_exscan(c[b], sh, total);
     }
-    if (r >= count) return;
-    const uint32_t total_items = blk[4 * nblocks];
-    if (total_items > item_cap) return;  // host re-plans with a larger workspace
+    if (r >= count || s.n == 0) return;
+    if (blk[kBins * nblocks] > item_cap) return;  // host re-plans with a larger workspace
     const uint32_t rid = uint32_t(r);
-    full_pos[r] = pos[0];
-    if (s.nfull > kLongChunks)
+    // bin 0 holds, in order: first (if bin 0), interior pieces, last (if bin 0)
+    const uint32_t b0 = piece_bin(s, 0);
+    const uint32_t fp = pos[b0]++;
+    items[fp] = piece_item(s, 0, rid);
+    first_pos[r] = fp;
+    if (s.n >= 2)
     {
-        // long record: its full-chunk items are written block-parallel by
-        // long_items_kernel and its chunks combined by long_finalize_kernel
-        longs[atomicAdd(const_cast<uint32_t*>(blk) + 4 * nblocks + 1, 1u)] = rid;
-    }
-    else
-        for (uint32_t j = 0; j < s.nfull; ++j) items[pos[0] + j] = full_item(s, rid, j);
-    if (s.hbin)
-    {
-        const uint32_t hp = s.hbin == 4 ? pos[0] + s.nfull : pos[4 - s.hbin];
-        Item it;
-        it.end = s.e - uint64_t(s.nfull) * kChunk;
-        it.len = s.rem;
-        it.rec_flag = rid | kItemStart;
-        items[hp] = it;
-        head_pos[r] = hp;
+        const uint32_t nint = s.n - 2;
+        int_pos[r] = pos[0];
+        if (nint > kLongChunks)
+            longs[atomicAdd(blk + kBins * nblocks + 1, 1u)] = rid;  // long_items_kernel
+        else
+            for (uint32_t i = 0; i < nint; ++i) items[pos[0] + i] = piece_item(s, 1 + i, rid);
+        pos[0] += nint;
+        const uint32_t b1 = piece_bin(s, s.n - 1);
+        const uint32_t lp = pos[b1];
+        items[lp] = piece_item(s, s.n - 1, rid);
+        last_pos[r] = lp;
     }
 }
 
-// Full-chunk items of long records, one workgroup per record.
+// Interior pieces of long records, one workgroup per record.
 __global__ __launch_bounds__(kLongBlock) void long_items_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ counters,
-    const uint32_t* __restrict__ longs, const uint32_t* __restrict__ full_pos,
+    const uint32_t* __restrict__ longs, const uint32_t* __restrict__ int_pos,
     Item* __restrict__ items, uint64_t item_cap)
 {
     if (counters[0] > item_cap) return;
@@ -568,9 +616,9 @@ __global__ __launch_bounds__(kLongBlock) void long_items_kernel(
     {
         const uint32_t r = longs[k];
         const RecShape s = rec_shape(uint64_t(base) + off[r], len[r]);
-        const uint32_t fp = full_pos[r];
-        for (uint32_t j = threadIdx.x; j < s.nfull; j += kLongBlock)
-            items[fp + j] = full_item(s, r, j);
+        const uint32_t ip = int_pos[r];
+        for (uint32_t i = threadIdx.x; i < s.n - 2; i += kLongBlock)
+            items[ip + i] = piece_item(s, 1 + i, r);
     }
 }
 
@@ -578,54 +626,56 @@ hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint
                            uint64_t count, const VarWorkspace& ws, hipStream_t stream)
 {
     const uint32_t nb = var_plan_blocks(count);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(nb), dim3(kPlanBlock), 0, stream,
-                       static_cast<const uint8_t*>(base), offsets, lengths, count, ws.blk, nb);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, 4 * nb);
-    hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanBlock), 0, stream,
-                       static_cast<const uint8_t*>(base), offsets, lengths, count, ws.blk, nb,
-                       ws.items, ws.item_cap, ws.full_pos, ws.head_pos, ws.longs);
-    hipLaunchKernelGGL(long_items_kernel, dim3(64), dim3(kLongBlock), 0, stream,
-                       static_cast<const uint8_t*>(base), offsets, lengths, ws.blk + 4 * nb,
-                       ws.longs, ws.full_pos, ws.items, ws.item_cap);
+    const uint8_t* b = static_cast<const uint8_t*>(base);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(nb), dim3(kPlanBlock), 0, stream, b, offsets,
+                       lengths, count, ws.blk, nb);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, kBins * nb);
+    hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanBlock), 0, stream, b, offsets,
+                       lengths, count, ws.blk, nb, ws.items, ws.item_cap, ws.first_pos,
+                       ws.int_pos, ws.last_pos, ws.longs);
+    hipLaunchKernelGGL(long_items_kernel, dim3(64), dim3(kLongBlock), 0, stream, b, offsets,
+                       lengths, ws.blk + kBins * nb, ws.longs, ws.int_pos, ws.items, ws.item_cap);
     return hipGetLastError();
 }
 
-// Zero every byte below the chunk start, branch-free; `o` = byte offset of
-// this lane's 16 B from the chunk start (rows with o <= -16 become zero).
-__device__ __forceinline__ uint4 mask_below_start(uint4 d, int32_t o)
+// Keep the bytes of this lane's 16 B whose offset from the piece start lies
+// in [0, hi), branch-free; `o` = offset of the 16 B.
+__device__ __forceinline__ uint4 mask_window(uint4 d, int32_t o, int32_t hi)
 {
     uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
     {
-        const int32_t below = -(o + 4 * q);  // bytes of this dword below the start
-        const uint32_t keep = below <= 0 ? 0xFFFFFFFFu
-                                         : (below >= 4 ? 0u : (0xFFFFFFFFu << (8 * below)));
-        w[q] &= keep;
+        const int32_t b0 = o + 4 * q;                            // offset of byte 0
+        const int32_t lo_cut = min(max(-b0, 0), 4);              // bytes below 0
+        const int32_t hi_cut = min(max(b0 + 4 - hi, 0), 4);      // bytes at or past hi
+        const uint32_t lo_keep = lo_cut >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo_cut));
+        const uint32_t hi_keep = hi_cut >= 4 ? 0u : (0xFFFFFFFFu >> (8 * hi_cut));
+        w[q] &= lo_keep & hi_keep;
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// One chunk as a team sees it: row 0 of group 0 of this lane starts at p0,
-// o0 bytes from the chunk start (negative = before it; such rows load from
-// `clamp`, a valid address in the chunk's first 16-byte block, and are
-// zeroed by head_fix).
+// One piece as a team sees it: row 0 of group 0 of this lane starts at p0,
+// o0 bytes from the piece start (negative = before it; such rows load from
+// the piece's first 16-byte block, p0 + coff, and are masked).
 struct ChunkView
 {
     const uint8_t* p0;
-    int32_t coff;  // clamp address - p0
+    int32_t coff;
     int32_t o0;
+    int32_t keep;  // bytes [0, keep) of the window from the piece start are data
 };
 
 template <int G>
 __device__ __forceinline__ ChunkView view_of(const Item& it, uint32_t tl)
 {
     ChunkView v;
-    const uint32_t len = it.len & kItemLenMask;
-    v.o0 = int32_t(len) - G * kGroupBytes + int32_t(tl) * 16;
-    v.p0 = reinterpret_cast<const uint8_t*>(it.end) - G * kGroupBytes + tl * 16;
-    // first 16-byte block of the chunk, relative to p0
-    v.coff = -v.o0 - int32_t((it.end - len) & 15u);
+    const int32_t lenw = int32_t(it.lenw_m & kItemLenMask);
+    v.keep = lenw - int32_t(it.lenw_m >> kItemMShift);
+    v.o0 = lenw - G * kGroupBytes + int32_t(tl) * 16;
+    v.p0 = reinterpret_cast<const uint8_t*>(it.wend) - G * kGroupBytes + tl * 16;
+    v.coff = -v.o0 - int32_t((it.wend - uint64_t(lenw)) & 15u);
     return v;
 }
 
@@ -633,10 +683,10 @@ __device__ __forceinline__ ChunkView view_of(const Item& it, uint32_t tl)
 // crc32c_fixed_pipe_kernel: every group's 8 loads are unconditional and
 // issued (sched_barrier) while the previous group is folded; item
 // descriptors run two items ahead, so the loop-carried loads are identical
-// on every path and vmcnt stays exact.  The init is not applied here (the
-// finalize kernels add Z_L(~init)); only head chunks, whose start is not on
-// the row grid, need masking, under a wave-uniform branch per group.  For
-// odd G two items are unrolled per iteration so the A/B buffers alternate.
+// on every path and vmcnt stays exact.  Masking (bytes before the piece, the
+// last piece's trailing bytes) happens only in groups where some team of the
+// wave needs it (a wave-uniform branch).  For odd G two items are unrolled
+// per iteration so the A/B buffers alternate.
 template <int G>
 __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32_t lo, uint32_t hi,
                                           uint32_t* __restrict__ partial, uint32_t team,
@@ -660,9 +710,13 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
         }
     };
 
+    // Descriptors run LA items ahead of the data: two for short pieces, one
+    // for 3-4 group pieces (whose own time covers the descriptor's latency;
+    // the extra registers would spill).
+    constexpr uint32_t LA = G >= 3 ? 1 : 2;
     uint4 A[kGroupRows], B[kGroupRows];
-    Item nit = items[idx_of(1)];  // descriptors run two items ahead of the data
     ChunkView cur = view_of<G>(items[idx_of(0)], tl);
+    Item nit = LA == 2 ? items[idx_of(1)] : Item{};
     load_group(A, cur, 0);
     uint32_t k = 0;
     for (uint32_t iter = 0; iter < iters; ++iter)
@@ -670,7 +724,8 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
 #pragma unroll
         for (int u = 0; u < U; ++u, ++k)
         {
-            const Item nnit = items[idx_of(k + 2)];
+            const Item nnit = items[idx_of(k + LA)];
+            if (LA == 1) nit = nnit;
             ChunkView nxt = cur;
             uint32_t V[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -688,11 +743,18 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 const int32_t og = cur.o0 + g * kGroupBytes;  // row 0 of this group
-                if (__builtin_amdgcn_ballot_w64(og < 0))     // some team starts in this group
+                const bool fix = og < 0 || (g == G - 1 && og + kGroupBytes - kRowBytes + 16 > cur.keep);
+                if (__builtin_amdgcn_ballot_w64(fix))
                 {
 #pragma unroll
                     for (int r = 0; r < kGroupRows; ++r)
-                        row_update(V, mask_below_start(bc[r], og + r * kRowBytes), li);
+                    {
+                        // rows before every team's piece start leave V = 0: skip them
+                        // (one-group pieces are sorted by row count, so this is common)
+                        if (G == 1 && !__builtin_amdgcn_ballot_w64(og + r * kRowBytes > -16))
+                            continue;
+                        row_update(V, mask_window(bc[r], og + r * kRowBytes, cur.keep), li);
+                    }
                 }
                 else
                 {
@@ -716,9 +778,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
     const Item* __restrict__ items, const uint32_t* __restrict__ blk, uint32_t nblocks,
     uint32_t* __restrict__ partial, uint64_t item_cap, const uint32_t* __restrict__ tables)
 {
-    const uint32_t n_items = blk[4 * nblocks];
+    const uint32_t n_items = blk[kBins * nblocks];
     if (n_items > item_cap) return;
-    // bin b (0..3 = 4, 3, 2, 1 groups) is [blk[b * nblocks], blk[(b + 1) * nblocks])
+    // bin b = 4 - G is [blk[b * nblocks], blk[(b + 1) * nblocks]); G = 1 takes
+    // bins 3..10 (one group, 8..1 rows) as one range
     const uint32_t b = 4 - G;
     const uint32_t lo = blk[b * nblocks];
     const uint32_t hi = b == 3 ? n_items : blk[(b + 1) * nblocks];
@@ -741,7 +804,8 @@ hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWor
                        ws.items, ws.blk, nb, ws.partial, ws.item_cap, tables)
     MI_LAUNCH_CHUNK(4);
     MI_LAUNCH_CHUNK(3);
-    MI_LAUNCH_CHUNK(2);  // bin 1 (heads <= 1 KiB) is hashed by the finalize kernel
+    MI_LAUNCH_CHUNK(2);
+    MI_LAUNCH_CHUNK(1);
 #undef MI_LAUNCH_CHUNK
     return hipGetLastError();
 }
@@ -753,106 +817,128 @@ __device__ __forceinline__ uint32_t zglob(const uint32_t* g, uint32_t v)
            g[768 + (v >> 24)];
 }
 
-// One thread per record: short records byte-serially; otherwise the
-// register after the head chunk when started from ~init -- hashed here for
-// heads <= kFinalizeHead (slice-by-16 over aligned 16-B loads), or
-// Z_rem(~init) ^ raw(head) from the chunk kernel (identity 1) -- carried over
-// the full chunks by Horner with Z_4096, then the < 16-byte tail.
-__global__ __launch_bounds__(256) void crc32c_finalize_kernel(
+// Z_n for n < 2^13 through the G^{2^k} tables.
+__device__ __forceinline__ uint32_t zbits(const uint32_t* p2, uint32_t v, uint32_t n)
+{
+    for (int k = 0; n; ++k, n >>= 1)
+        if (n & 1u) v = zglob(p2 + k * 1024, v);
+    return v;
+}
+
+// Z_{-m}, 0 <= m < 128: Z_{-128} o Z_{128-m}.
+__device__ __forceinline__ uint32_t zneg(const uint32_t* p2, const uint32_t* zinv, uint32_t v,
+                                        uint32_t m)
+{
+    return m ? zglob(zinv, zbits(p2, v, kRowBytes - m)) : v;
+}
+
+// Register after a record's first piece when started from `x`.
+__device__ __forceinline__ uint32_t first_piece_state(const RecShape& s, const uint32_t* p2,
+                                                      const uint32_t* zinv, uint32_t x,
+                                                      uint32_t R0)
+{
+    // window [.., w), piece [a, pe), m = w - pe: R0 = Z_m(raw(piece));
+    // state = Z_{pe-a}(x) ^ raw(piece) = Z_{-m}(Z_{w-a}(x) ^ R0)
+    const uint64_t pe = piece_end(s, 0);
+    const uint64_t w = (pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
+    return zneg(p2, zinv, zbits(p2, x, uint32_t(w - s.a)) ^ R0, uint32_t(w - pe));
+}
+
+// Register after the last piece (n >= 2) from the state before it.
+__device__ __forceinline__ uint32_t last_piece_state(const RecShape& s, const uint32_t* p2,
+                                                     const uint32_t* zinv, uint32_t x,
+                                                     uint32_t R)
+{
+    const uint64_t ps = piece_start(s, s.n - 1), pe = s.E;
+    const uint64_t w = (pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
+    return zneg(p2, zinv, zbits(p2, x, uint32_t(w - ps)) ^ R, uint32_t(w - pe));
+}
+
+// One thread per record: Horner from ~init over its pieces (see the section
+// comment); records < 32 B byte-serially.
+__global__ __launch_bounds__(512) void crc32c_finalize_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
-    const uint32_t* __restrict__ partial, const uint32_t* __restrict__ full_pos,
-    const uint32_t* __restrict__ head_pos, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables)
+    const uint32_t* __restrict__ partial, const uint32_t* __restrict__ first_pos,
+    const uint32_t* __restrict__ int_pos, const uint32_t* __restrict__ last_pos,
+    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables)
 {
-    __shared__ uint32_t T[16][256];
+    __shared__ uint32_t t0[256];
     __shared__ uint32_t zc[1024];
-    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) T[i / 256][i % 256] = tables[kTabT + i];
-    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) zc[i] = tables[kTabZChunk + i];
+    __shared__ uint32_t zinv[1024];
+    __shared__ uint32_t p2[13 * 1024];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) t0[i] = tables[kTabT + i];
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x)
+    {
+        zc[i] = tables[kTabZChunk + i];
+        zinv[i] = tables[kTabZInv128 + i];
+    }
+    for (uint32_t i = threadIdx.x; i < 13 * 1024; i += blockDim.x) p2[i] = tables[kTabP2 + i];
     __syncthreads();
     const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (r >= count) return;
     const uint8_t* p = base + off[r];
     const uint32_t L = len[r];
-    const uint32_t x = ~(inits ? inits[r] : 0u);
+    uint32_t c = ~(inits ? inits[r] : 0u);
     const RecShape s = rec_shape(uint64_t(p), L);
-    uint32_t c = x;
-    uint64_t tail_from = 0;
-    if (L >= uint32_t(kSmallRecord))
+    if (s.n == 0)
     {
-        if (s.nfull > kLongChunks) return;  // long_finalize_kernel
-        if (s.hbin)
-        {
-            const uint32_t* p2 = tables + kTabP2;  // L2-resident G^{2^b}
-            for (int b = 0; b < 12; ++b)
-                if (s.rem & (1u << b)) c = zglob(p2 + b * 1024, c);
-            c ^= partial[head_pos[r]];
-        }
-        else if (s.rem)
-        {
-            // head [p, p + rem): bytes up to 16-byte alignment, then slice-by-16
-            const uint8_t* q = p;
-            const uint8_t* hend = p + s.rem;  // 16-aligned
-            while ((uintptr_t(q) & 15u) && q < hend) c = T[0][(c ^ *q++) & 0xFFu] ^ (c >> 8);
-            for (; q < hend; q += 16)
-            {
-                const uint4 w = *reinterpret_cast<const uint4*>(q);
-                const uint32_t a = c ^ w.x;
-                c = T[15][a & 0xFFu] ^ T[14][(a >> 8) & 0xFFu] ^ T[13][(a >> 16) & 0xFFu] ^
-                    T[12][a >> 24] ^ T[11][w.y & 0xFFu] ^ T[10][(w.y >> 8) & 0xFFu] ^
-                    T[9][(w.y >> 16) & 0xFFu] ^ T[8][w.y >> 24] ^ T[7][w.z & 0xFFu] ^
-                    T[6][(w.z >> 8) & 0xFFu] ^ T[5][(w.z >> 16) & 0xFFu] ^ T[4][w.z >> 24] ^
-                    T[3][w.w & 0xFFu] ^ T[2][(w.w >> 8) & 0xFFu] ^ T[1][(w.w >> 16) & 0xFFu] ^
-                    T[0][w.w >> 24];
-            }
-        }
-        const uint32_t fp = full_pos[r];
-        for (uint32_t j = s.nfull; j-- > 0;) c = zglob(zc, c) ^ partial[fp + j];
-        tail_from = s.e - uint64_t(p);
+        for (uint32_t i = 0; i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
     }
-    for (uint64_t i = tail_from; i < L; ++i) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+    else
+    {
+        if (s.n >= 2 && s.n - 2 > kLongChunks) return;  // long_finalize_kernel
+        c = first_piece_state(s, p2, zinv, c, partial[first_pos[r]]);
+        if (s.n >= 2)
+        {
+            const uint32_t ip = int_pos[r];
+            for (uint32_t j = 0; j + 2 < s.n; ++j) c = zglob(zc, c) ^ partial[ip + j];
+            c = last_piece_state(s, p2, zinv, c, partial[last_pos[r]]);
+        }
+    }
     out[r] = ~c;
 }
 
-// Long records: raw(main) = Z_{C nfull}(head) ^ XOR_j Z_{C j}(p_j), j counted
-// from the end.  Thread t folds chunks j = t + 1024 k by Horner with
-// Z_{1024 C}, shifts its sum by Z_{C t} (bits of t, tables G^{C 2^b}), and
-// the workgroup XOR-reduces; thread 0 adds the head chunk, the tail bytes
-// and the final inversion.
+// Long records (> kLongChunks interior pieces): the interior run contributes
+// XOR_jj Z_{C jj}(p[ip + nint - 1 - jj]).  Thread t folds jj = t + 1024 q by
+// Horner with Z_{1024 C}, shifts by Z_{C t} (tables G^{C 2^b}) and the
+// workgroup XOR-reduces; thread 0 adds the first piece carried by
+// Z_{C nint} and the last piece.
 __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits,
     const uint32_t* __restrict__ counters, const uint32_t* __restrict__ longs,
-    const uint32_t* __restrict__ partial, const uint32_t* __restrict__ full_pos,
-    const uint32_t* __restrict__ head_pos, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint64_t item_cap)
+    const uint32_t* __restrict__ partial, const uint32_t* __restrict__ first_pos,
+    const uint32_t* __restrict__ int_pos, const uint32_t* __restrict__ last_pos,
+    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
+    const uint32_t* __restrict__ pow2, uint64_t item_cap)
 {
-    __shared__ uint32_t t0[256];
     __shared__ uint32_t zs[1024];
     __shared__ uint32_t zc2[10][1024];
     __shared__ uint32_t red[kLongBlock / 64];
     if (counters[0] > item_cap) return;
     const uint32_t nlong = counters[1];
     if (blockIdx.x >= nlong) return;
-    for (uint32_t i = threadIdx.x; i < 256; i += kLongBlock) t0[i] = tables[kTabT + i];
     for (uint32_t i = threadIdx.x; i < 1024; i += kLongBlock) zs[i] = tables[kTabZLong + i];
     for (uint32_t i = threadIdx.x; i < 10 * 1024; i += kLongBlock)
         zc2[i / 1024][i % 1024] = tables[kTabZC2 + i];
     __syncthreads();
     const uint32_t t = threadIdx.x;
+    const uint32_t* p2 = tables + kTabP2;
+    const uint32_t* zinv = tables + kTabZInv128;
     for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x)
     {
         const uint32_t r = longs[k];
         const uint8_t* p = base + off[r];
-        const uint32_t L = len[r];
-        const RecShape s = rec_shape(uint64_t(p), L);
-        const uint32_t fp = full_pos[r];
+        const RecShape s = rec_shape(uint64_t(p), len[r]);
+        const uint32_t nint = s.n - 2;
+        const uint32_t ip = int_pos[r];
         uint32_t acc = 0;
-        if (t < s.nfull)
+        if (t < nint)
         {
-            const uint32_t n_t = (s.nfull - t + kLongBlock - 1) / kLongBlock;
+            const uint32_t n_t = (nint - t + kLongBlock - 1) / kLongBlock;
             for (uint32_t q = n_t; q-- > 0;)
-                acc = zglob(zs, acc) ^ partial[fp + t + q * kLongBlock];
+                acc = zglob(zs, acc) ^ partial[ip + nint - 1 - (t + q * kLongBlock)];
             for (int b = 0; b < 10; ++b)
                 if (t & (1u << b)) acc = zglob(zc2[b], acc);
         }
@@ -863,23 +949,13 @@ __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
         {
             uint32_t c = 0;
             for (int w = 0; w < kLongBlock / 64; ++w) c ^= red[w];
-            // register after the head chunk when started from ~init (see the
-            // finalize kernel), carried over the full chunks by Z_{C nfull}
-            uint32_t h = ~(inits ? inits[r] : 0u);
-            if (s.hbin)
-            {
-                for (int b = 0; b < 12; ++b)
-                    if (s.rem & (1u << b)) h = zglob(pow2 + b * 1024, h);
-                h ^= partial[head_pos[r]];
-            }
-            else
-                for (uint32_t i = 0; i < s.rem; ++i) h = t0[(h ^ p[i]) & 0xFFu] ^ (h >> 8);
-            uint64_t n = uint64_t(s.nfull) * kChunk;  // bytes after the head chunk
+            uint32_t h = first_piece_state(s, p2, zinv, ~(inits ? inits[r] : 0u),
+                                           partial[first_pos[r]]);
+            uint64_t n = uint64_t(nint) * kChunk;  // bytes of the interior run
             for (int b = 0; n && b < 48; ++b, n >>= 1)
                 if (n & 1u) h = zglob(pow2 + b * 1024, h);
             c ^= h;
-            for (uint64_t i = s.e - uint64_t(p); i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
-            out[r] = ~c;
+            out[r] = ~last_piece_state(s, p2, zinv, c, partial[last_pos[r]]);
         }
         __syncthreads();
     }
@@ -891,15 +967,14 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
                                hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
-    const uint32_t nb = uint32_t((count + 255) / 256);
-    hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(nb), dim3(256), 0, stream,
-                       static_cast<const uint8_t*>(base), offsets, lengths, inits, count,
-                       ws.partial, ws.full_pos, ws.head_pos, out, tables);
+    const uint8_t* b = static_cast<const uint8_t*>(base);
+    hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(uint32_t((count + 511) / 512)), dim3(512), 0,
+                       stream, b, offsets, lengths, inits, count, ws.partial, ws.first_pos,
+                       ws.int_pos, ws.last_pos, out, tables);
     const uint32_t grid = uint32_t(count < 256 ? count : 256);
-    hipLaunchKernelGGL(long_finalize_kernel, dim3(grid), dim3(kLongBlock), 0, stream,
-                       static_cast<const uint8_t*>(base), offsets, lengths, inits,
-                       ws.blk + 4 * var_plan_blocks(count), ws.longs, ws.partial, ws.full_pos,
-                       ws.head_pos, out, tables, pow2, ws.item_cap);
+    hipLaunchKernelGGL(long_finalize_kernel, dim3(grid), dim3(kLongBlock), 0, stream, b, offsets,
+                       lengths, inits, ws.blk + kBins * var_plan_blocks(count), ws.longs, ws.partial,
+                       ws.first_pos, ws.int_pos, ws.last_pos, out, tables, pow2, ws.item_cap);
     return hipGetLastError();
 }
 
@@ -977,7 +1052,8 @@ hipError_t configure_kernels()
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     const void* c[] = {reinterpret_cast<const void*>(&crc32c_chunk_kernel<4>),
                        reinterpret_cast<const void*>(&crc32c_chunk_kernel<3>),
-                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<2>)};
+                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<2>),
+                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<1>)};
     for (const void* f : c)
         if (e == hipSuccess)
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);

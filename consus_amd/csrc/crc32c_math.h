@@ -64,6 +64,46 @@ struct Op32
     }
 };
 
+// Inverse of an invertible operator (Gauss-Jordan over GF(2)).  Z_n is
+// invertible because x is a unit modulo the CRC polynomial.  Returns false if
+// the matrix is singular.
+inline bool invert(const Op32& m, Op32* inv)
+{
+    // rows[i] = (row i of M) | (row i of I) << 32, bit j of the low half = M[i][j]
+    uint64_t rows[32];
+    for (int i = 0; i < 32; ++i)
+    {
+        uint64_t r = 0;
+        for (int j = 0; j < 32; ++j)
+            if ((m.col[j] >> i) & 1u) r |= uint64_t(1) << j;
+        rows[i] = r | (uint64_t(1) << (32 + i));
+    }
+    for (int c = 0; c < 32; ++c)
+    {
+        int piv = -1;
+        for (int i = c; i < 32; ++i)
+            if ((rows[i] >> c) & 1u)
+            {
+                piv = i;
+                break;
+            }
+        if (piv < 0) return false;
+        const uint64_t t = rows[c];
+        rows[c] = rows[piv];
+        rows[piv] = t;
+        for (int i = 0; i < 32; ++i)
+            if (i != c && ((rows[i] >> c) & 1u)) rows[i] ^= rows[c];
+    }
+    for (int j = 0; j < 32; ++j)
+    {
+        uint32_t col = 0;
+        for (int i = 0; i < 32; ++i)
+            if ((rows[i] >> (32 + j)) & 1u) col |= 1u << i;
+        inv->col[j] = col;
+    }
+    return true;
+}
+
 // Z_n by square-and-multiply over the 2^k-byte operators.
 inline Op32 zeros_op(uint64_t nbytes)
 {
@@ -80,12 +120,17 @@ inline Op32 zeros_op(uint64_t nbytes)
 
 inline uint32_t shift_bytes(uint32_t s, uint64_t nbytes) { return zeros_op(nbytes).apply(s); }
 
-// G^n_j[b] = Z_n(b << 8j), j = 0..3 -- four 256-entry tables.
-inline void make_fold_tables(uint32_t out[4][256], uint64_t nbytes)
+// Operator tables: out[j][b] = z(b << 8j), j = 0..3 -- four 256-entry tables.
+inline void make_op_tables(uint32_t out[4][256], const Op32& z)
 {
-    const Op32 z = zeros_op(nbytes);
     for (int j = 0; j < 4; ++j)
         for (uint32_t b = 0; b < 256; ++b) out[j][b] = z.apply(b << (8 * j));
+}
+
+// G^n_j[b] = Z_n(b << 8j).
+inline void make_fold_tables(uint32_t out[4][256], uint64_t nbytes)
+{
+    make_op_tables(out, zeros_op(nbytes));
 }
 
 // Slice-by-16 tables T_0..T_15.

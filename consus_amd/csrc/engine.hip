@@ -94,9 +94,18 @@ int init_device(int device)
     for (int b = 0; b < 10; ++b)
         make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZC2 + b * 1024]),
                          uint64_t(kChunk) << b);
-    for (int b = 0; b < 12; ++b)
+    for (int b = 0; b < 13; ++b)
         make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabP2 + b * 1024]),
                          uint64_t(1) << b);
+    {
+        Op32 inv;
+        if (!invert(zeros_op(kRowBytes), &inv))
+        {
+            delete d;
+            return fail(MI_CRC32C_EHIP, "Z_128 is not invertible (table construction bug)");
+        }
+        make_op_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZInv128]), inv);
+    }
     std::vector<uint32_t> pow2(48 * 1024);
     Op32 p = Op32::zero_byte();
     for (int k = 0; k < 64; ++k)
@@ -178,7 +187,7 @@ struct Ctx
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     DevBuf data, off, len, inits, out;  // staging of host batches
-    DevBuf items, partial, full_pos, head_pos, blk, longs;
+    DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     PinBuf pin_small;                   // plan-size read-back, small host outputs
 
     int open(int ordinal)
@@ -227,9 +236,9 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
     if (count >= (1ull << 31)) return fail(MI_CRC32C_EINVAL, "count >= 2^31 records");
     const uint32_t nb = var_plan_blocks(count);
     int st;
-    if ((st = c->blk.reserve((4 * size_t(nb) + 4) * 4)) ||
-        (st = c->full_pos.reserve(count * 4)) || (st = c->head_pos.reserve(count * 4)) ||
-        (st = c->longs.reserve(count * 4)))
+    if ((st = c->blk.reserve((kBins * size_t(nb) + 4) * 4)) ||
+        (st = c->first_pos.reserve(count * 4)) || (st = c->int_pos.reserve(count * 4)) ||
+        (st = c->last_pos.reserve(count * 4)) || (st = c->longs.reserve(count * 4)))
         return st;
     uint64_t cap = total_bytes ? total_bytes / kChunk + 2 * uint64_t(count) + 1
                                : std::max<uint64_t>(c->items.cap / sizeof(Item), 2 * count + 1);
@@ -239,14 +248,15 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
         if ((st = c->items.reserve(cap * sizeof(Item))) || (st = c->partial.reserve(cap * 4)))
             return st;
         cap = std::min<uint64_t>(c->items.cap / sizeof(Item), c->partial.cap / 4);
-        VarWorkspace ws{c->blk.as<uint32_t>(), c->items.as<Item>(), c->partial.as<uint32_t>(),
-                        c->full_pos.as<uint32_t>(), c->head_pos.as<uint32_t>(),
-                        c->longs.as<uint32_t>(), cap};
+        VarWorkspace ws{c->blk.as<uint32_t>(),       c->items.as<Item>(),
+                        c->partial.as<uint32_t>(),   c->first_pos.as<uint32_t>(),
+                        c->int_pos.as<uint32_t>(),   c->last_pos.as<uint32_t>(),
+                        c->longs.as<uint32_t>(),     cap};
         HIP_TRY(launch_var_plan(base, off, len, count, ws, c->stream));
         if (!total_bytes)
         {
             uint32_t* h = c->pin_small.as<uint32_t>();
-            HIP_TRY(hipMemcpyAsync(h, c->blk.as<uint32_t>() + 4 * nb, 4, hipMemcpyDeviceToHost,
+            HIP_TRY(hipMemcpyAsync(h, c->blk.as<uint32_t>() + kBins * nb, 4, hipMemcpyDeviceToHost,
                                    c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
             if (*h > cap)
@@ -662,8 +672,8 @@ int mi_crc32c_pipeline_destroy(mi_crc32c_pipeline* p)
             (void)hipStreamSynchronize(s.ctx.stream);
         }
         for (DevBuf* b : {&s.ctx.data, &s.ctx.off, &s.ctx.len, &s.ctx.inits, &s.ctx.out,
-                          &s.ctx.items, &s.ctx.partial, &s.ctx.full_pos, &s.ctx.head_pos,
-                          &s.ctx.blk, &s.ctx.longs, &s.dseg, &s.dmeta})
+                          &s.ctx.items, &s.ctx.partial, &s.ctx.first_pos, &s.ctx.int_pos,
+                          &s.ctx.last_pos, &s.ctx.blk, &s.ctx.longs, &s.dseg, &s.dmeta})
             if (b->p) (void)hipFree(b->p);
         for (PinBuf* b : {&s.ctx.pin_small, &s.seg, &s.meta, &s.res})
             if (b->p) (void)hipHostFree(b->p);
