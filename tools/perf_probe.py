@@ -3,6 +3,8 @@ import sys, time, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import consus_amd as E
+if len(sys.argv) > 2:
+    E.LIB_PATH = os.path.abspath(sys.argv[2])  # A/B builds (tools/ab.py)
 
 count = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 L = 4096

@@ -69,6 +69,32 @@ __global__ __launch_bounds__(1024, 1) void probe_team(const uint8_t* __restrict_
     if (acc == 0x12345678u) sink[threadIdx.x] = acc;
 }
 
+// TEAM-lane teams: rows of 16*TEAM bytes, record stride 4 KiB, 16 loads per step.
+template <int TEAM>
+__global__ __launch_bounds__(1024, 1) void probe_teamN(const uint8_t* __restrict__ base,
+                                                       uint64_t count, uint32_t* __restrict__ sink)
+{
+    constexpr int ROW = 16 * TEAM;
+    const uint32_t tl = threadIdx.x & (TEAM - 1);
+    const uint64_t team = (uint64_t(blockIdx.x) * 1024 + threadIdx.x) / TEAM;
+    const uint64_t nteams = uint64_t(gridDim.x) * 1024 / TEAM;
+    uint32_t acc = 0;
+    for (uint64_t rec = team; rec < count; rec += nteams)
+    {
+        const uint8_t* r = base + rec * 4096 + tl * 16;
+        for (int g = 0; g < 4096 / ROW; g += 16)
+        {
+            uint4 v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                v[k] = ld<true>(reinterpret_cast<const uint4*>(r + (g + k) * ROW));
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+        }
+    }
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid, int reps,
@@ -90,6 +116,10 @@ extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid,
             case 5: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096 - 1, sink, 16u); break;
             case 6: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096 - 1, sink, 64u); break;
             case 7: hipLaunchKernelGGL((probe_team<true>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096 - 1, sink, 80u); break;
+            case 8: hipLaunchKernelGGL((probe_teamN<4>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+            case 9: hipLaunchKernelGGL((probe_teamN<8>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+            case 10: hipLaunchKernelGGL((probe_teamN<16>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+            case 11: hipLaunchKernelGGL((probe_teamN<2>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
         }
     };
     launch();

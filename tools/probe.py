@@ -22,9 +22,11 @@ buf = E.DeviceBuffer(nbytes)
 buf.fill_splitmix64(0xC0DE)
 sink = E.DeviceBuffer(4096 * 4)
 names = {0: "stream plain U8", 1: "stream nt U8", 2: "stream plain U16", 3: "team plain",
-         4: "team nt", 5: "team nt skew16", 6: "team nt skew64", 7: "team nt skew80"}
+         4: "team nt", 5: "team nt skew16", 6: "team nt skew64", 7: "team nt skew80",
+         8: "team4 nt", 9: "team8 nt", 10: "team16 nt", 11: "team2 nt"}
 for which, grids in ((0, (2048, 4096, 8192)), (1, (2048, 4096, 8192)), (2, (2048, 4096)),
-                     (3, (256,)), (4, (256,)), (5, (256,)), (6, (256,)), (7, (256,))):
+                     (3, (256,)), (4, (256,)), (5, (256,)), (6, (256,)), (7, (256,)),
+                     (8, (256,)), (9, (256,)), (10, (256,)), (11, (256,)), (4, (256,))):
     for g in grids:
         ms = P.probe_run(which, C.c_void_p(buf.ptr), nbytes, g, 10, C.c_void_p(sink.ptr))
         print(f"{names[which]:18s} grid {g:5d}: {ms:.4f} ms  {nbytes / ms / 1e6:8.1f} GB/s "
