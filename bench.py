@@ -49,7 +49,8 @@ METRIC = "GiB/s CRC32C over device-resident 4 KiB records; % of HBM read peak"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E datasheet peak (MI355X_MICROARCH.md)
 SEED = 0xC0DE
 RECORD = 4096
-KERNEL_NAME = "crc32c_fixed_kernel"
+KERNEL_NAME = "crc32c_fixed_pipe_kernel"  # 4 KiB records: G = 4 groups, no inits
+KERNEL_MATCH = "crc32c_fixed"             # PMC rows: either fixed-length kernel
 
 
 def parse():
@@ -101,7 +102,7 @@ def pmc_traffic(args) -> tuple[float | None, str]:
     for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if KERNEL_NAME in row.get("Kernel_Name", "") and \
+                if KERNEL_MATCH in row.get("Kernel_Name", "") and \
                         row.get("Counter_Name") == "FETCH_SIZE":
                     vals.append(float(row["Counter_Value"]))
     shutil.rmtree(out, ignore_errors=True)

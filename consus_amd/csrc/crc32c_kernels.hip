@@ -159,7 +159,11 @@ __device__ __forceinline__ uint4 load16(const uint8_t* p)
         const uint32_t a = uint32_t(uintptr_t(p));
         return make_uint4(a, a * 3u, a ^ 0x55u, a + 7u);
     }
-    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    // explicitly global: a pointer rebuilt from an integer (Item::wend) would
+    // otherwise be FLAT, and FLAT loads also count in lgkmcnt, so every wait
+    // for an LDS lookup would drain the prefetched rows too
+    typedef const __attribute__((address_space(1))) u32x4_t* gptr;
+    const u32x4_t v = __builtin_nontemporal_load((gptr)(uintptr_t)p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -875,28 +879,31 @@ __global__ __launch_bounds__(512) void crc32c_finalize_kernel(
     }
     for (uint32_t i = threadIdx.x; i < 13 * 1024; i += blockDim.x) p2[i] = tables[kTabP2 + i];
     __syncthreads();
-    const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (r >= count) return;
-    const uint8_t* p = base + off[r];
-    const uint32_t L = len[r];
-    uint32_t c = ~(inits ? inits[r] : 0u);
-    const RecShape s = rec_shape(uint64_t(p), L);
-    if (s.n == 0)
+    // persistent grid: the tables are staged once per workgroup
+    for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < count;
+         r += uint64_t(gridDim.x) * blockDim.x)
     {
-        for (uint32_t i = 0; i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
-    }
-    else
-    {
-        if (s.n >= 2 && s.n - 2 > kLongChunks) return;  // long_finalize_kernel
-        c = first_piece_state(s, p2, zinv, c, partial[first_pos[r]]);
-        if (s.n >= 2)
+        const uint8_t* p = base + off[r];
+        const uint32_t L = len[r];
+        uint32_t c = ~(inits ? inits[r] : 0u);
+        const RecShape s = rec_shape(uint64_t(p), L);
+        if (s.n == 0)
         {
-            const uint32_t ip = int_pos[r];
-            for (uint32_t j = 0; j + 2 < s.n; ++j) c = zglob(zc, c) ^ partial[ip + j];
-            c = last_piece_state(s, p2, zinv, c, partial[last_pos[r]]);
+            for (uint32_t i = 0; i < L; ++i) c = t0[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
         }
+        else
+        {
+            if (s.n >= 2 && s.n - 2 > kLongChunks) continue;  // long_finalize_kernel
+            c = first_piece_state(s, p2, zinv, c, partial[first_pos[r]]);
+            if (s.n >= 2)
+            {
+                const uint32_t ip = int_pos[r];
+                for (uint32_t j = 0; j + 2 < s.n; ++j) c = zglob(zc, c) ^ partial[ip + j];
+                c = last_piece_state(s, p2, zinv, c, partial[last_pos[r]]);
+            }
+        }
+        out[r] = ~c;
     }
-    out[r] = ~c;
 }
 
 // Long records (> kLongChunks interior pieces): the interior run contributes
@@ -968,7 +975,10 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
 {
     if (count == 0) return hipSuccess;
     const uint8_t* b = static_cast<const uint8_t*>(base);
-    hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(uint32_t((count + 511) / 512)), dim3(512), 0,
+    // two 512-thread workgroups per CU fit the 62 KB of tables each stages
+    const uint64_t fin_blocks = (count + 511) / 512;
+    hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(uint32_t(fin_blocks < 512 ? fin_blocks : 512)),
+                       dim3(512), 0,
                        stream, b, offsets, lengths, inits, count, ws.partial, ws.first_pos,
                        ws.int_pos, ws.last_pos, out, tables);
     const uint32_t grid = uint32_t(count < 256 ? count : 256);

@@ -1,17 +1,21 @@
-"""A/B the fixed-length kernel across library builds (dev tool).
+"""A/B library builds (dev tool).
 
-python tools/ab.py LIB_A.so LIB_B.so ...  -- each build is timed in its own
-process, interleaved over three rounds, with tools/perf_probe.py.
+python tools/ab.py [--zipf] LIB_A.so LIB_B.so ...  -- each build is timed in
+its own process, interleaved over three rounds, with tools/perf_probe.py
+(1M x 4 KiB records) or tools/zipf_probe.py (config 3).
 """
 import os
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-libs = sys.argv[1:]
+args = sys.argv[1:]
+zipf = "--zipf" in args
+libs = [a for a in args if a != "--zipf"]
 for rnd in range(3):
     for lib in libs:
-        r = subprocess.run([sys.executable, os.path.join(HERE, "perf_probe.py"), str(1 << 20), lib],
-                           capture_output=True, text=True, timeout=120)
+        cmd = [sys.executable, os.path.join(HERE, "zipf_probe.py"), lib] if zipf else \
+              [sys.executable, os.path.join(HERE, "perf_probe.py"), str(1 << 20), lib]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
         line = (r.stdout.strip().splitlines() or ["<no output> " + r.stderr[-300:]])[-1]
         print(f"round {rnd} {os.path.basename(lib):28s} {line}", flush=True)
