@@ -338,3 +338,33 @@ class Pipeline:
             self.close()
         except Exception:
             pass
+
+
+# ---- RCCL communicator (one process per GPU) --------------------
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId on this rank (send it to the others over any control plane)."""
+    buf = (C.c_ubyte * COMM_ID_BYTES)()
+    _check(lib().mi_comm_unique_id(buf), "mi_comm_unique_id")
+    return bytes(buf)
+
+
+def comm_init(unique_id: bytes, nranks: int, rank: int) -> None:
+    if len(unique_id) != COMM_ID_BYTES:
+        raise ValueError("unique id must be COMM_ID_BYTES long")
+    buf = (C.c_ubyte * COMM_ID_BYTES).from_buffer_copy(unique_id)
+    _check(lib().mi_comm_init(buf, nranks, rank), "mi_comm_init")
+
+
+def comm_allgather_u32(send: DeviceBuffer, count: int, recv: DeviceBuffer) -> None:
+    """All-gather `count` u32 per rank into recv (nranks * count u32), synchronous."""
+    if send.nbytes < 4 * count:
+        raise ValueError("send buffer too small")
+    _check(lib().mi_comm_allgather_u32(C.c_void_p(send.ptr), count, C.c_void_p(recv.ptr)),
+           "mi_comm_allgather_u32")
+
+
+def comm_destroy() -> None:
+    _check(lib().mi_comm_destroy(), "mi_comm_destroy")

@@ -165,3 +165,24 @@ def test_large_single_buffer(engine, oracle):
     buf = rng.integers(0, 256, (1 << 30) + 12345, dtype=np.uint8)
     for n in (buf.size, (1 << 30), 3 << 28):
         assert engine.crc32c(0x1234, buf[:n]) == oracle.crc32c(0x1234, buf, n)
+
+
+def test_rccl_single_rank_allgather(engine, oracle):
+    """The RCCL communicator (mi_comm_*) on one rank: the gathered CRC vector
+    is the rank's own, and a second init is refused until destroy."""
+    count = 4096
+    data = engine.DeviceBuffer(count * 256)
+    data.fill_splitmix64(0x1)
+    out, recv = engine.DeviceBuffer(count * 4), engine.DeviceBuffer(count * 4)
+    engine.device_batch_fixed(data, 256, 256, count, out)
+    uid = engine.comm_unique_id()
+    engine.comm_init(uid, 1, 0)
+    try:
+        with pytest.raises(engine.EngineError):
+            engine.comm_init(uid, 1, 0)
+        engine.comm_allgather_u32(out, count, recv)
+        got = recv.download(np.uint32, count)
+        assert np.array_equal(got, out.download(np.uint32, count))
+        assert np.array_equal(got, oracle.fixed(data.download(np.uint8), 256, 256, count))
+    finally:
+        engine.comm_destroy()
