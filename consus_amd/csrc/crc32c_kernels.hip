@@ -642,60 +642,82 @@ hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint
     return hipGetLastError();
 }
 
-// Keep the bytes of this lane's 16 B whose offset from the piece start lies
-// in [0, hi), branch-free; `o` = offset of the 16 B.
-__device__ __forceinline__ uint4 mask_window(uint4 d, int32_t o, int32_t hi)
+// Byte masks of one 16-B block, word q: keep bytes >= b (b in 0..16) or
+// bytes < c (c in 0..16).  64-bit shifts make the 0- and 32-bit edge cases
+// branch-free (a shift by 32 empties the word).
+__device__ __forceinline__ uint32_t keep_from(int32_t b, int q)
 {
-    uint32_t w[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-    {
-        const int32_t b0 = o + 4 * q;                            // offset of byte 0
-        const int32_t lo_cut = min(max(-b0, 0), 4);              // bytes below 0
-        const int32_t hi_cut = min(max(b0 + 4 - hi, 0), 4);      // bytes at or past hi
-        const uint32_t lo_keep = lo_cut >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo_cut));
-        const uint32_t hi_keep = hi_cut >= 4 ? 0u : (0xFFFFFFFFu >> (8 * hi_cut));
-        w[q] &= lo_keep & hi_keep;
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    const uint32_t s = uint32_t(min(max(b - 4 * q, 0), 4)) * 8u;
+    return uint32_t(~uint64_t(0) << s);
 }
 
-// One piece as a team sees it: row 0 of group 0 of this lane starts at p0,
-// o0 bytes from the piece start (negative = before it; such rows load from
-// the piece's first 16-byte block, p0 + coff, and are masked).
+__device__ __forceinline__ uint32_t keep_below(int32_t c, int q)
+{
+    const uint32_t s = uint32_t(min(max(c - 4 * q, 0), 4)) * 8u;
+    return uint32_t((uint64_t(0xFFFFFFFFu) << s) >> 32);
+}
+
+__device__ __forceinline__ uint4 mask_from(uint4 d, int32_t b)
+{
+    return make_uint4(d.x & keep_from(b, 0), d.y & keep_from(b, 1), d.z & keep_from(b, 2),
+                      d.w & keep_from(b, 3));
+}
+
+__device__ __forceinline__ uint4 mask_below(uint4 d, int32_t c)
+{
+    return make_uint4(d.x & keep_below(c, 0), d.y & keep_below(c, 1), d.z & keep_below(c, 2),
+                      d.w & keep_below(c, 3));
+}
+
+// One piece as a lane sees it.  Window coordinates: the window is G groups
+// of 8 rows ending at the item's 128-aligned end; the piece occupies window
+// bytes [s0, G*1024 - m).
+//   p0   this lane's 16 B of window row 0
+//   x    16*lane - s0: offset of that block from the piece start.  A block of
+//        group 0 lying wholly before the piece is loaded from a zero block
+//        instead (no read before the piece, nothing to mask).
+//   rsb  the one row/byte where the piece starts inside this lane's block
+//        ((row << 4) | byte, or 0xFF..: none): that block keeps bytes >= byte
+//   ce   bytes of this lane's block in the LAST row that belong to the
+//        piece (0..16); the rest is masked
 struct ChunkView
 {
     const uint8_t* p0;
-    int32_t coff;
-    int32_t o0;
-    int32_t keep;  // bytes [0, keep) of the window from the piece start are data
+    int32_t x;
+    int32_t rsb;
+    int32_t ce;
 };
 
 template <int G>
 __device__ __forceinline__ ChunkView view_of(const Item& it, uint32_t tl)
 {
-    ChunkView v;
+    constexpr int32_t W = G * int32_t(kGroupBytes);
     const int32_t lenw = int32_t(it.lenw_m & kItemLenMask);
-    v.keep = lenw - int32_t(it.lenw_m >> kItemMShift);
-    v.o0 = lenw - G * kGroupBytes + int32_t(tl) * 16;
-    v.p0 = reinterpret_cast<const uint8_t*>(it.wend) - G * kGroupBytes + tl * 16;
-    v.coff = -v.o0 - int32_t((it.wend - uint64_t(lenw)) & 15u);
+    const int32_t m = int32_t(it.lenw_m >> kItemMShift);
+    const int32_t s0 = W - lenw;
+    ChunkView v;
+    v.p0 = reinterpret_cast<const uint8_t*>(it.wend) - W + tl * 16;
+    v.x = int32_t(tl) * 16 - s0;
+    v.rsb = ((s0 & 15) != 0 && ((s0 >> 4) & 7) == int32_t(tl)) ? (((s0 >> 7) << 4) | (s0 & 15))
+                                                               : 0x7FFFFFFF;
+    v.ce = min(max(W - m - (W - int32_t(kRowBytes)) - int32_t(tl) * 16, 0), 16);
     return v;
 }
 
 // Items [lo, hi) all have G groups (the plan bins them).  Same discipline as
 // crc32c_fixed_pipe_kernel: every group's 8 loads are unconditional and
 // issued (sched_barrier) while the previous group is folded; item
-// descriptors run two items ahead, so the loop-carried loads are identical
-// on every path and vmcnt stays exact.  Masking (bytes before the piece, the
-// last piece's trailing bytes) happens only in groups where some team of the
-// wave needs it (a wave-uniform branch).  For odd G two items are unrolled
+// descriptors run ahead, so the loop-carried loads are identical on every
+// path and vmcnt stays exact.  Masking is per block, not per row: group-0
+// blocks before the piece read zeros, the start block is masked only in the
+// row where some team of the wave has one (a wave-uniform ballot), and the
+// last row is masked to the piece end.  For odd G two items are unrolled
 // per iteration so the A/B buffers alternate.
 template <int G>
 __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32_t lo, uint32_t hi,
                                           uint32_t* __restrict__ partial, uint32_t team,
                                           uint32_t team0, uint32_t nteams, uint32_t tl,
-                                          uint32_t li)
+                                          uint32_t li, const uint8_t* zero16)
 {
     if (hi <= lo || lo + team0 >= hi) return;
     constexpr int U = (G % 2 == 0) ? 1 : 2;  // items per loop iteration
@@ -709,8 +731,11 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
 #pragma unroll
         for (int r = 0; r < kGroupRows; ++r)
         {
-            const int32_t o = v.o0 + g * kGroupBytes + r * kRowBytes;
-            buf[r] = load16(v.p0 + (o > -16 ? g * kGroupBytes + r * kRowBytes : v.coff));
+            const int32_t o = g * int32_t(kGroupBytes) + r * int32_t(kRowBytes);
+            if (g == 0)
+                buf[r] = load16(v.x + o > -16 ? v.p0 + o : zero16);
+            else
+                buf[r] = load16(v.p0 + o);
         }
     };
 
@@ -746,24 +771,22 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
                     load_group(bn, nxt, 0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                const int32_t og = cur.o0 + g * kGroupBytes;  // row 0 of this group
-                const bool fix = og < 0 || (g == G - 1 && og + kGroupBytes - kRowBytes + 16 > cur.keep);
-                if (__builtin_amdgcn_ballot_w64(fix))
-                {
 #pragma unroll
-                    for (int r = 0; r < kGroupRows; ++r)
+                for (int r = 0; r < kGroupRows; ++r)
+                {
+                    uint4 d = bc[r];
+                    if (g == 0)
                     {
-                        // rows before every team's piece start leave V = 0: skip them
+                        // rows before every team's piece leave V = 0: skip them
                         // (one-group pieces are sorted by row count, so this is common)
-                        if (G == 1 && !__builtin_amdgcn_ballot_w64(og + r * kRowBytes > -16))
+                        if (G == 1 && !__builtin_amdgcn_ballot_w64(cur.x + r * int32_t(kRowBytes) > -16))
                             continue;
-                        row_update(V, mask_window(bc[r], og + r * kRowBytes, cur.keep), li);
+                        const bool start_here = (cur.rsb >> 4) == r;
+                        if (__builtin_amdgcn_ballot_w64(start_here))
+                            d = mask_from(d, start_here ? (cur.rsb & 15) : 0);
                     }
-                }
-                else
-                {
-#pragma unroll
-                    for (int r = 0; r < kGroupRows; ++r) row_update(V, bc[r], li);
+                    if (g == G - 1 && r == kGroupRows - 1) d = mask_below(d, cur.ce);
+                    row_update(V, d, li);
                 }
             }
             const uint32_t raw = team_fold(V);
@@ -794,7 +817,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
     if (hi <= lo || lo + (blockIdx.x * kBlock) / kTeam >= hi) return;  // whole workgroup idle
     stage_tables(tables);
     const uint32_t tl = threadIdx.x & (kTeam - 1);
-    chunk_bin<G>(items, lo, hi, partial, team, team & ~7u, nteams, tl, lane_info());
+    chunk_bin<G>(items, lo, hi, partial, team, team & ~7u, nteams, tl, lane_info(),
+                 reinterpret_cast<const uint8_t*>(tables + kTabZero));
 }
 
 hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
