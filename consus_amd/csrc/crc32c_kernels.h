@@ -46,14 +46,15 @@ constexpr uint32_t kLdsBytes = kLdsZ64 + 4096;  // 155648
 // 4 KiB-aligned chunk of the address space.  A team hashes the 128-B-aligned
 // window [wend - G KiB, wend), wend = the piece end rounded up to 128, with
 // the bytes before the piece start and the m bytes after its end masked.
+// Packed in 8 bytes: wend >> 7 (41 bits: addresses below 2^48), the window
+// length wend - piece start (13 bits, <= 4096 + 127) and m (7 bits).
 struct Item
 {
-    uint64_t wend;
-    uint32_t lenw_m;  // (wend - piece start) | m << kItemMShift
-    uint32_t rec;
+    uint64_t bits;
 };
-constexpr uint32_t kItemMShift = 16;
-constexpr uint32_t kItemLenMask = 0xFFFFu;
+constexpr uint32_t kItemAddrShift = 20;
+constexpr uint32_t kItemLenShift = 7;
+constexpr uint64_t kItemMaxAddr = uint64_t(1) << 48;
 
 hipError_t configure_kernels();
 
@@ -64,7 +65,7 @@ hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const u
 // Variable-length pipeline.  `ws_*` are engine-owned device workspaces.
 struct VarWorkspace
 {
-    uint32_t* blk;        // kBins * nblocks + 4 u32 (bin counts -> offsets, then totals)
+    uint32_t* blk;        // kBins * nblocks block counts, then the plan header (plan_hdr)
     Item* items;          // capacity `item_cap`
     uint32_t* partial;    // capacity `item_cap`
     uint32_t* first_pos;  // count: item of the record's first piece
@@ -83,6 +84,10 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
                                uint32_t* out, const uint32_t* tables, const uint32_t* pow2,
                                hipStream_t stream);
 uint32_t var_plan_blocks(uint64_t count);
+// Plan header after the kBins x blocks counts: bin starts, total items, long records.
+constexpr uint32_t kPlanHdrTotal = kBins;
+constexpr uint32_t kPlanHdrWords = kBins + 4;
+inline uint32_t* plan_hdr(uint32_t* blk, uint32_t nblocks) { return blk + kBins * nblocks; }
 
 hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,
                           uint64_t count, uint32_t* out, const uint32_t* pow2_tables,

@@ -159,7 +159,7 @@ __device__ __forceinline__ uint4 load16(const uint8_t* p)
         const uint32_t a = uint32_t(uintptr_t(p));
         return make_uint4(a, a * 3u, a ^ 0x55u, a + 7u);
     }
-    // explicitly global: a pointer rebuilt from an integer (Item::wend) would
+    // explicitly global: a pointer rebuilt from an integer (Item::bits) would
     // otherwise be FLAT, and FLAT loads also count in lgkmcnt, so every wait
     // for an LDS lookup would drain the prefetched rows too
     typedef const __attribute__((address_space(1))) u32x4_t* gptr;
@@ -389,11 +389,24 @@ hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const u
 //             undoing the last piece's m trailing zeros with
 //             Z_{-m} = Z_{-128} o Z_{128-m}; records < 32 B byte-serially.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPlanBlock = 256;
+// Plan blocks: 1024 threads x 4 consecutive records.  The per-block bin
+// counts live in blk[bin * nblocks + block]; the plan header follows them
+// (plan_hdr): bin starts [0, kBins), total items, long-record count.
+constexpr uint32_t kPlanThreads = 1024;
+constexpr uint32_t kPlanPer = 4;
+constexpr uint32_t kPlanRecs = kPlanThreads * kPlanPer;
+constexpr uint32_t kHdrTotal = kPlanHdrTotal;
+constexpr uint32_t kHdrLongs = kBins + 1;
+static_assert(kHdrLongs < kPlanHdrWords, "plan header size");
 
 uint32_t var_plan_blocks(uint64_t count)
 {
-    return uint32_t((count + kPlanBlock - 1) / kPlanBlock);
+    return uint32_t((count + kPlanRecs - 1) / kPlanRecs);
+}
+
+__device__ __forceinline__ uint32_t* plan_hdr_d(uint32_t* blk, uint32_t nblocks)
+{
+    return blk + kBins * nblocks;
 }
 
 struct RecShape
@@ -422,15 +435,22 @@ __device__ __forceinline__ uint64_t piece_end(const RecShape& s, uint32_t i)
     return c < s.E ? c : s.E;
 }
 
-__device__ __forceinline__ Item piece_item(const RecShape& s, uint32_t i, uint32_t rec)
+__device__ __forceinline__ Item make_item(uint64_t w, uint32_t lenw, uint32_t m)
+{
+    return Item{((w >> 7) << kItemAddrShift) | (uint64_t(lenw) << kItemLenShift) | m};
+}
+
+__device__ __forceinline__ Item piece_item(const RecShape& s, uint32_t i)
 {
     const uint64_t ps = piece_start(s, i), pe = piece_end(s, i);
     const uint64_t w = (pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
-    Item it;
-    it.wend = w;
-    it.lenw_m = uint32_t(w - ps) | (uint32_t(w - pe) << kItemMShift);
-    it.rec = rec;
-    return it;
+    return make_item(w, uint32_t(w - ps), uint32_t(w - pe));
+}
+
+// Interior piece j (0-based) of a record whose first piece is in chunk k0.
+__device__ __forceinline__ Item interior_item(uint64_t k0, uint32_t j)
+{
+    return make_item((k0 + 2 + j) * kChunk, kChunk, 0);
 }
 
 // bins 0, 1, 2 = 4, 3, 2 groups of 8 rows; 3 + (8 - R) = one group, R rows
@@ -442,11 +462,9 @@ __device__ __forceinline__ uint32_t piece_bin(const RecShape& s, uint32_t i)
     return rows > kGroupRows ? 4 - (rows + kGroupRows - 1) / kGroupRows : 3 + (kGroupRows - rows);
 }
 
-// items per bin for one record: first, interior (bin 0), last
-__device__ __forceinline__ void rec_counts(const RecShape& s, uint32_t c[kBins])
+// items per bin for one record, added to c: first, interior (bin 0), last
+__device__ __forceinline__ void rec_counts_add(const RecShape& s, uint32_t c[kBins])
 {
-#pragma unroll
-    for (uint32_t b = 0; b < kBins; ++b) c[b] = 0;
     if (s.n == 0) return;
     c[piece_bin(s, 0)] += 1;
     if (s.n >= 2)
@@ -456,154 +474,191 @@ __device__ __forceinline__ void rec_counts(const RecShape& s, uint32_t c[kBins])
     }
 }
 
-// Block-wide exclusive scan of one u32 per thread (kPlanBlock threads).
-__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t& total)
+// Bin counts packed for block-wide sums/scans: bin 0 in its own word (a
+// block holds < 2^32 pieces of it), bins 1..10 two per word in 16-bit fields
+// (a record adds at most 2 to a bin: <= 8192 per block).
+constexpr int kPacked = 6;
+
+__device__ __forceinline__ void pack_counts(const uint32_t c[kBins], uint32_t p[kPacked])
 {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t x = v;
+    p[0] = c[0];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1)
-    {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= uint32_t(d)) x += y;
-    }
-    if (lane == 63) sh[wave] = x;
-    __syncthreads();
-    uint32_t woff = 0;
-    total = 0;
-    for (uint32_t w = 0; w < kPlanBlock / 64; ++w)
-    {
-        if (w < wave) woff += sh[w];
-        total += sh[w];
-    }
-    __syncthreads();
-    return woff + x - v;
+    for (int w = 1; w < kPacked; ++w) p[w] = c[2 * w - 1] | (c[2 * w] << 16);
 }
 
-__global__ __launch_bounds__(kPlanBlock) void plan_count_kernel(
+__device__ __forceinline__ void unpack_counts(const uint32_t p[kPacked], uint32_t c[kBins])
+{
+    c[0] = p[0];
+#pragma unroll
+    for (int w = 1; w < kPacked; ++w)
+    {
+        c[2 * w - 1] = p[w] & 0xFFFFu;
+        c[2 * w] = p[w] >> 16;
+    }
+}
+
+__global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, uint64_t count, uint32_t* __restrict__ blk, uint32_t nblocks)
 {
-    __shared__ uint32_t sh[kPlanBlock / 64];
-    const uint64_t r = uint64_t(blockIdx.x) * kPlanBlock + threadIdx.x;
+    __shared__ uint32_t sh[kPlanThreads / 64][kPacked];
+    const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kPlanPer;
     uint32_t c[kBins] = {};
-    if (r < count) rec_counts(rec_shape(uint64_t(base) + off[r], len[r]), c);
 #pragma unroll
-    for (uint32_t b = 0; b < kBins; ++b)
-    {
-        uint32_t total;
-        block_exscan(c[b], sh, total);
-        if (threadIdx.x == 0) blk[b * nblocks + blockIdx.x] = total;
-    }
-}
-
-// Single-workgroup exclusive scan over n u32 (in place), in LDS tiles of
-// 16K entries loaded and stored coalesced; each thread scans 16 consecutive
-// entries of the tile (index padded by one word per 32 against bank
-// conflicts).  Writes the grand total to blk[n] and zeroes the long-record
-// counter blk[n + 1].
-constexpr uint32_t kScanPer = 16;
-constexpr uint32_t kScanTile = 1024 * kScanPer;
-
-__device__ __forceinline__ uint32_t scan_slot(uint32_t i) { return i + (i >> 5); }
-
-__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ blk, uint32_t n)
-{
-    __shared__ uint32_t tile[kScanTile + kScanTile / 32];
-    __shared__ uint32_t sh[16];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
+    for (uint32_t q = 0; q < kPlanPer; ++q)
+        if (r0 + q < count) rec_counts_add(rec_shape(uint64_t(base) + off[r0 + q], len[r0 + q]), c);
+    uint32_t p[kPacked];
+    pack_counts(c, p);
+#pragma unroll
+    for (int w = 0; w < kPacked; ++w)
+        for (int d = 32; d >= 1; d >>= 1) p[w] += __shfl_xor(p[w], d);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    for (uint32_t base = 0; base < n; base += kScanTile)
-    {
-        const uint32_t cnt = min(kScanTile, n - base);
-        for (uint32_t i = threadIdx.x; i < kScanTile; i += 1024)
-            tile[scan_slot(i)] = i < cnt ? blk[base + i] : 0u;
-        __syncthreads();
-        uint32_t v[kScanPer], sum = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kScanPer; ++j)
-        {
-            v[j] = tile[scan_slot(threadIdx.x * kScanPer + j)];
-            sum += v[j];
-        }
-        uint32_t x = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1)
-        {
-            const uint32_t y = __shfl_up(x, d);
-            if (lane >= uint32_t(d)) x += y;
-        }
-        if (lane == 63) sh[wave] = x;
-        __syncthreads();
-        uint32_t run = carry + x - sum, tot = 0;
-        for (uint32_t w = 0; w < 16; ++w)
-        {
-            if (w < wave) run += sh[w];
-            tot += sh[w];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kScanPer; ++j)
-        {
-            tile[scan_slot(threadIdx.x * kScanPer + j)] = run;
-            run += v[j];
-        }
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < cnt; i += 1024) blk[base + i] = tile[scan_slot(i)];
-        if (threadIdx.x == 0) carry += tot;
-        __syncthreads();
-    }
+    if (lane == 0)
+        for (int w = 0; w < kPacked; ++w) sh[wave][w] = p[w];
+    __syncthreads();
     if (threadIdx.x == 0)
     {
-        blk[n] = carry;  // total items
-        blk[n + 1] = 0;  // long-record list length (plan_scatter appends)
+        uint32_t t[kPacked] = {};
+        for (uint32_t v = 0; v < kPlanThreads / 64; ++v)
+            for (int w = 0; w < kPacked; ++w) t[w] += sh[v][w];
+        uint32_t tc[kBins];
+        unpack_counts(t, tc);
+        for (uint32_t b = 0; b < kBins; ++b) blk[b * nblocks + blockIdx.x] = tc[b];
+        if (blockIdx.x == 0) plan_hdr_d(blk, nblocks)[kHdrLongs] = 0;  // plan_scatter appends
     }
 }
 
-__global__ __launch_bounds__(kPlanBlock) void plan_scatter_kernel(
+// Each block finds its own base in every bin from the per-block counts (no
+// separate scan pass): wave b < kBins sums bin b over all blocks and over the
+// blocks before this one.  Block 0 publishes the plan header.
+__global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, uint64_t count, uint32_t* __restrict__ blk,
     uint32_t nblocks, Item* __restrict__ items, uint64_t item_cap,
     uint32_t* __restrict__ first_pos, uint32_t* __restrict__ int_pos,
     uint32_t* __restrict__ last_pos, uint32_t* __restrict__ longs)
 {
-    __shared__ uint32_t sh[kPlanBlock / 64];
-    const uint64_t r = uint64_t(blockIdx.x) * kPlanBlock + threadIdx.x;
-    RecShape s{0, 0, 0, 0};
+    __shared__ uint32_t tot[kBins], pre[kBins], bin_base[kBins];
+    __shared__ uint32_t total_items;
+    __shared__ uint32_t sh[kPlanThreads / 64][kPacked];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (wave < kBins)
+    {
+        uint32_t t = 0, before = 0;
+        for (uint32_t b = lane; b < nblocks; b += 64)
+        {
+            const uint32_t v = blk[wave * nblocks + b];
+            t += v;
+            before += b < blockIdx.x ? v : 0u;
+        }
+        for (int d = 32; d >= 1; d >>= 1)
+        {
+            t += __shfl_xor(t, d);
+            before += __shfl_xor(before, d);
+        }
+        if (lane == 0)
+        {
+            tot[wave] = t;
+            pre[wave] = before;
+        }
+    }
+
+    // this thread's records and their counts (overlaps the loads above)
+    const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kPlanPer;
+    RecShape sh_rec[kPlanPer];
     uint32_t c[kBins] = {};
-    if (r < count)
-    {
-        s = rec_shape(uint64_t(base) + off[r], len[r]);
-        rec_counts(s, c);
-    }
-    uint32_t pos[kBins];
 #pragma unroll
-    for (uint32_t b = 0; b < kBins; ++b)
+    for (uint32_t q = 0; q < kPlanPer; ++q)
     {
-        uint32_t total;
-        pos[b] = blk[b * nblocks + blockIdx.x] + block_exscan(c[b], sh, total);
+        sh_rec[q] = RecShape{0, 0, 0, 0};
+        if (r0 + q < count)
+        {
+            sh_rec[q] = rec_shape(uint64_t(base) + off[r0 + q], len[r0 + q]);
+            rec_counts_add(sh_rec[q], c);
+        }
     }
-    if (r >= count || s.n == 0) return;
-    if (blk[kBins * nblocks] > item_cap) return;  // host re-plans with a larger workspace
-    const uint32_t rid = uint32_t(r);
-    // bin 0 holds, in order: first (if bin 0), interior pieces, last (if bin 0)
-    const uint32_t b0 = piece_bin(s, 0);
-    const uint32_t fp = pos[b0]++;
-    items[fp] = piece_item(s, 0, rid);
-    first_pos[r] = fp;
-    if (s.n >= 2)
+    // block exclusive scan of the packed counts
+    uint32_t p[kPacked], x[kPacked];
+    pack_counts(c, p);
+#pragma unroll
+    for (int w = 0; w < kPacked; ++w)
     {
-        const uint32_t nint = s.n - 2;
-        int_pos[r] = pos[0];
-        if (nint > kLongChunks)
-            longs[atomicAdd(blk + kBins * nblocks + 1, 1u)] = rid;  // long_items_kernel
-        else
-            for (uint32_t i = 0; i < nint; ++i) items[pos[0] + i] = piece_item(s, 1 + i, rid);
-        pos[0] += nint;
-        const uint32_t b1 = piece_bin(s, s.n - 1);
-        const uint32_t lp = pos[b1];
-        items[lp] = piece_item(s, s.n - 1, rid);
-        last_pos[r] = lp;
+        x[w] = p[w];
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            const uint32_t y = __shfl_up(x[w], d);
+            if (lane >= uint32_t(d)) x[w] += y;
+        }
+    }
+    if (lane == 63)
+        for (int w = 0; w < kPacked; ++w) sh[wave][w] = x[w];
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        uint32_t run = 0;
+        for (uint32_t b = 0; b < kBins; ++b)
+        {
+            bin_base[b] = run + pre[b];
+            if (blockIdx.x == 0) plan_hdr_d(blk, nblocks)[b] = run;
+            run += tot[b];
+        }
+        total_items = run;
+        if (blockIdx.x == 0) plan_hdr_d(blk, nblocks)[kHdrTotal] = run;
+    }
+    uint32_t ex[kPacked];
+#pragma unroll
+    for (int w = 0; w < kPacked; ++w)
+    {
+        uint32_t acc = x[w] - p[w];
+        for (uint32_t v = 0; v < wave; ++v) acc += sh[v][w];
+        ex[w] = acc;
+    }
+    __syncthreads();
+    if (total_items > item_cap) return;  // host re-plans with a larger workspace
+    uint32_t pos[kBins];
+    unpack_counts(ex, pos);
+#pragma unroll
+    for (uint32_t b = 0; b < kBins; ++b) pos[b] += bin_base[b];
+
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q)
+    {
+        const RecShape& s = sh_rec[q];
+        const uint64_t r = r0 + q;
+        uint32_t nint_w = 0, ip = 0;  // interior run this lane hands to its wave
+        if (r < count && s.n != 0)
+        {
+            // bin 0 holds, in order: first (if bin 0), interior pieces, last (if bin 0)
+            const uint32_t fp = pos[piece_bin(s, 0)]++;
+            items[fp] = piece_item(s, 0);
+            first_pos[r] = fp;
+            if (s.n >= 2)
+            {
+                const uint32_t nint = s.n - 2;
+                ip = pos[0];
+                int_pos[r] = ip;
+                if (nint > kLongChunks)
+                    longs[atomicAdd(plan_hdr_d(blk, nblocks) + kHdrLongs, 1u)] = uint32_t(r);
+                else
+                    nint_w = nint;
+                pos[0] += nint;
+                const uint32_t lp = pos[piece_bin(s, s.n - 1)]++;
+                items[lp] = piece_item(s, s.n - 1);
+                last_pos[r] = lp;
+            }
+        }
+        // interior runs: the whole wave writes each lane's run, 64 items per store
+        uint64_t pending = __builtin_amdgcn_ballot_w64(nint_w != 0);
+        while (pending)
+        {
+            const int l = __builtin_ctzll(pending);
+            pending &= pending - 1;
+            const uint32_t n_l = __shfl(nint_w, l);
+            const uint32_t ip_l = __shfl(ip, l);
+            const uint64_t k0_l = uint64_t(__shfl(uint32_t(s.k0), l)) |
+                                  (uint64_t(__shfl(uint32_t(s.k0 >> 32), l)) << 32);
+            for (uint32_t j = lane; j < n_l; j += 64) items[ip_l + j] = interior_item(k0_l, j);
+        }
     }
 }
 
@@ -614,15 +669,15 @@ __global__ __launch_bounds__(kLongBlock) void long_items_kernel(
     const uint32_t* __restrict__ longs, const uint32_t* __restrict__ int_pos,
     Item* __restrict__ items, uint64_t item_cap)
 {
-    if (counters[0] > item_cap) return;
-    const uint32_t nlong = counters[1];
+    if (counters[kHdrTotal] > item_cap) return;
+    const uint32_t nlong = counters[kHdrLongs];
     for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x)
     {
         const uint32_t r = longs[k];
         const RecShape s = rec_shape(uint64_t(base) + off[r], len[r]);
         const uint32_t ip = int_pos[r];
         for (uint32_t i = threadIdx.x; i < s.n - 2; i += kLongBlock)
-            items[ip + i] = piece_item(s, 1 + i, r);
+            items[ip + i] = interior_item(s.k0, i);
     }
 }
 
@@ -631,14 +686,13 @@ hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint
 {
     const uint32_t nb = var_plan_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(nb), dim3(kPlanBlock), 0, stream, b, offsets,
+    hipLaunchKernelGGL(plan_count_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, count, ws.blk, nb);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, kBins * nb);
-    hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanBlock), 0, stream, b, offsets,
+    hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, count, ws.blk, nb, ws.items, ws.item_cap, ws.first_pos,
                        ws.int_pos, ws.last_pos, ws.longs);
     hipLaunchKernelGGL(long_items_kernel, dim3(64), dim3(kLongBlock), 0, stream, b, offsets,
-                       lengths, ws.blk + kBins * nb, ws.longs, ws.int_pos, ws.items, ws.item_cap);
+                       lengths, plan_hdr(ws.blk, nb), ws.longs, ws.int_pos, ws.items, ws.item_cap);
     return hipGetLastError();
 }
 
@@ -692,11 +746,11 @@ template <int G>
 __device__ __forceinline__ ChunkView view_of(const Item& it, uint32_t tl)
 {
     constexpr int32_t W = G * int32_t(kGroupBytes);
-    const int32_t lenw = int32_t(it.lenw_m & kItemLenMask);
-    const int32_t m = int32_t(it.lenw_m >> kItemMShift);
+    const int32_t lenw = int32_t((it.bits >> kItemLenShift) & 0x1FFFu);
+    const int32_t m = int32_t(it.bits & 0x7Fu);
     const int32_t s0 = W - lenw;
     ChunkView v;
-    v.p0 = reinterpret_cast<const uint8_t*>(it.wend) - W + tl * 16;
+    v.p0 = reinterpret_cast<const uint8_t*>((it.bits >> kItemAddrShift) << 7) - W + tl * 16;
     v.x = int32_t(tl) * 16 - s0;
     v.rsb = ((s0 & 15) != 0 && ((s0 >> 4) & 7) == int32_t(tl)) ? (((s0 >> 7) << 4) | (s0 & 15))
                                                                : 0x7FFFFFFF;
@@ -805,13 +859,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
     const Item* __restrict__ items, const uint32_t* __restrict__ blk, uint32_t nblocks,
     uint32_t* __restrict__ partial, uint64_t item_cap, const uint32_t* __restrict__ tables)
 {
-    const uint32_t n_items = blk[kBins * nblocks];
+    const uint32_t* hdr = blk + kBins * nblocks;  // plan_hdr
+    const uint32_t n_items = hdr[kHdrTotal];
     if (n_items > item_cap) return;
-    // bin b = 4 - G is [blk[b * nblocks], blk[(b + 1) * nblocks]); G = 1 takes
-    // bins 3..10 (one group, 8..1 rows) as one range
+    // bin b = 4 - G is [hdr[b], hdr[b + 1]); G = 1 takes bins 3..10 (one
+    // group, 8..1 rows) as one range
     const uint32_t b = 4 - G;
-    const uint32_t lo = blk[b * nblocks];
-    const uint32_t hi = b == 3 ? n_items : blk[(b + 1) * nblocks];
+    const uint32_t lo = hdr[b];
+    const uint32_t hi = b == 3 ? n_items : hdr[b + 1];
     const uint32_t team = (blockIdx.x * kBlock + threadIdx.x) / kTeam;
     const uint32_t nteams = gridDim.x * kBlock / kTeam;
     if (hi <= lo || lo + (blockIdx.x * kBlock) / kTeam >= hi) return;  // whole workgroup idle
@@ -947,8 +1002,8 @@ __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
     __shared__ uint32_t zs[1024];
     __shared__ uint32_t zc2[10][1024];
     __shared__ uint32_t red[kLongBlock / 64];
-    if (counters[0] > item_cap) return;
-    const uint32_t nlong = counters[1];
+    if (counters[kHdrTotal] > item_cap) return;
+    const uint32_t nlong = counters[kHdrLongs];
     if (blockIdx.x >= nlong) return;
     for (uint32_t i = threadIdx.x; i < 1024; i += kLongBlock) zs[i] = tables[kTabZLong + i];
     for (uint32_t i = threadIdx.x; i < 10 * 1024; i += kLongBlock)
@@ -1007,7 +1062,7 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
                        ws.int_pos, ws.last_pos, out, tables);
     const uint32_t grid = uint32_t(count < 256 ? count : 256);
     hipLaunchKernelGGL(long_finalize_kernel, dim3(grid), dim3(kLongBlock), 0, stream, b, offsets,
-                       lengths, inits, ws.blk + kBins * var_plan_blocks(count), ws.longs, ws.partial,
+                       lengths, inits, plan_hdr(ws.blk, var_plan_blocks(count)), ws.longs, ws.partial,
                        ws.first_pos, ws.int_pos, ws.last_pos, out, tables, pow2, ws.item_cap);
     return hipGetLastError();
 }

@@ -234,9 +234,12 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
 {
     if (count == 0) return MI_CRC32C_OK;
     if (count >= (1ull << 31)) return fail(MI_CRC32C_EINVAL, "count >= 2^31 records");
+    // items pack addresses in 41 bits (crc32c_kernels.h: Item); user-space and
+    // GPU virtual addresses are below 2^47
+    if (uintptr_t(base) >= (kItemMaxAddr >> 1)) return fail(MI_CRC32C_EINVAL, "address above 2^47");
     const uint32_t nb = var_plan_blocks(count);
     int st;
-    if ((st = c->blk.reserve((kBins * size_t(nb) + 4) * 4)) ||
+    if ((st = c->blk.reserve((kBins * size_t(nb) + kPlanHdrWords) * 4)) ||
         (st = c->first_pos.reserve(count * 4)) || (st = c->int_pos.reserve(count * 4)) ||
         (st = c->last_pos.reserve(count * 4)) || (st = c->longs.reserve(count * 4)))
         return st;
@@ -256,8 +259,8 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
         if (!total_bytes)
         {
             uint32_t* h = c->pin_small.as<uint32_t>();
-            HIP_TRY(hipMemcpyAsync(h, c->blk.as<uint32_t>() + kBins * nb, 4, hipMemcpyDeviceToHost,
-                                   c->stream));
+            HIP_TRY(hipMemcpyAsync(h, plan_hdr(c->blk.as<uint32_t>(), nb) + kPlanHdrTotal, 4,
+                                   hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
             if (*h > cap)
             {
