@@ -33,7 +33,8 @@ constexpr int kTabZC2 = kTabZLong + 1024;      // G^{4096*2^b}, b = 0..9
 constexpr int kTabP2 = kTabZC2 + 10 * 1024;    // G^{2^k}, k = 0..12 (shifts up to 4 KiB)
 constexpr int kTabZInv128 = kTabP2 + 13 * 1024; // Z_{-128} = (Z_128)^{-1}
 constexpr int kTabZero = kTabZInv128 + 1024;    // 4 zero words (init 0 when inits == nullptr)
-constexpr int kTabWords = kTabZero + 4;
+constexpr int kTabFInit = kTabZero + 4;         // Z_n(0xFFFFFFFF), n = 0..4096 (init 0 seeds)
+constexpr int kTabWords = kTabFInit + 4097;
 
 // LDS image of the record kernels (bytes).
 constexpr uint32_t kLdsMain = 0;            // 128 KiB bank-private G^{128}

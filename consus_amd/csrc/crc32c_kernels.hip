@@ -462,28 +462,45 @@ __device__ __forceinline__ uint32_t piece_bin(const RecShape& s, uint32_t i)
     return rows > kGroupRows ? 4 - (rows + kGroupRows - 1) / kGroupRows : 3 + (kGroupRows - rows);
 }
 
-// items per bin for one record, added to c: first, interior (bin 0), last
-__device__ __forceinline__ void rec_counts_add(const RecShape& s, uint32_t c[kBins])
+// One thread's bin counts over its kPlanPer records without dynamically
+// indexed arrays: bin 0 in c0, bins 1..10 in 4-bit fields of cn (a record
+// adds at most 2 to a bin, so a thread's count is <= 8).
+struct ThreadCounts
 {
-    if (s.n == 0) return;
-    c[piece_bin(s, 0)] += 1;
-    if (s.n >= 2)
+    uint32_t c0 = 0;
+    uint64_t cn = 0;
+    __device__ void add(uint32_t bin)
     {
-        c[0] += s.n - 2;
-        c[piece_bin(s, s.n - 1)] += 1;
+        if (bin == 0)
+            c0 += 1;
+        else
+            cn += uint64_t(1) << (4 * (bin - 1));
     }
-}
+    // first, interior (bin 0), last
+    __device__ void add_record(const RecShape& s)
+    {
+        if (s.n == 0) return;
+        add(piece_bin(s, 0));
+        if (s.n >= 2)
+        {
+            c0 += s.n - 2;
+            add(piece_bin(s, s.n - 1));
+        }
+    }
+};
 
 // Bin counts packed for block-wide sums/scans: bin 0 in its own word (a
 // block holds < 2^32 pieces of it), bins 1..10 two per word in 16-bit fields
-// (a record adds at most 2 to a bin: <= 8192 per block).
+// (<= 8 per thread: <= 8192 per block).
 constexpr int kPacked = 6;
 
-__device__ __forceinline__ void pack_counts(const uint32_t c[kBins], uint32_t p[kPacked])
+__device__ __forceinline__ void pack_counts(const ThreadCounts& t, uint32_t p[kPacked])
 {
-    p[0] = c[0];
+    p[0] = t.c0;
 #pragma unroll
-    for (int w = 1; w < kPacked; ++w) p[w] = c[2 * w - 1] | (c[2 * w] << 16);
+    for (int w = 1; w < kPacked; ++w)
+        p[w] = uint32_t((t.cn >> (8 * (w - 1))) & 0xFu) |
+               (uint32_t((t.cn >> (8 * (w - 1) + 4)) & 0xFu) << 16);
 }
 
 __device__ __forceinline__ void unpack_counts(const uint32_t p[kPacked], uint32_t c[kBins])
@@ -503,12 +520,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
 {
     __shared__ uint32_t sh[kPlanThreads / 64][kPacked];
     const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kPlanPer;
-    uint32_t c[kBins] = {};
+    ThreadCounts tc;
 #pragma unroll
     for (uint32_t q = 0; q < kPlanPer; ++q)
-        if (r0 + q < count) rec_counts_add(rec_shape(uint64_t(base) + off[r0 + q], len[r0 + q]), c);
+        if (r0 + q < count) tc.add_record(rec_shape(uint64_t(base) + off[r0 + q], len[r0 + q]));
     uint32_t p[kPacked];
-    pack_counts(c, p);
+    pack_counts(tc, p);
 #pragma unroll
     for (int w = 0; w < kPacked; ++w)
         for (int d = 32; d >= 1; d >>= 1) p[w] += __shfl_xor(p[w], d);
@@ -521,9 +538,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
         uint32_t t[kPacked] = {};
         for (uint32_t v = 0; v < kPlanThreads / 64; ++v)
             for (int w = 0; w < kPacked; ++w) t[w] += sh[v][w];
-        uint32_t tc[kBins];
-        unpack_counts(t, tc);
-        for (uint32_t b = 0; b < kBins; ++b) blk[b * nblocks + blockIdx.x] = tc[b];
+        uint32_t bc[kBins];
+        unpack_counts(t, bc);
+        for (uint32_t b = 0; b < kBins; ++b) blk[b * nblocks + blockIdx.x] = bc[b];
         if (blockIdx.x == 0) plan_hdr_d(blk, nblocks)[kHdrLongs] = 0;  // plan_scatter appends
     }
 }
@@ -540,6 +557,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
 {
     __shared__ uint32_t tot[kBins], pre[kBins], bin_base[kBins];
     __shared__ uint32_t total_items;
+    __shared__ uint32_t slot[kBins][kPlanThreads];
     __shared__ uint32_t sh[kPlanThreads / 64][kPacked];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     if (wave < kBins)
@@ -565,21 +583,21 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
 
     // this thread's records and their counts (overlaps the loads above)
     const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kPlanPer;
-    RecShape sh_rec[kPlanPer];
-    uint32_t c[kBins] = {};
+    RecShape srec[kPlanPer];
+    ThreadCounts tc;
 #pragma unroll
     for (uint32_t q = 0; q < kPlanPer; ++q)
     {
-        sh_rec[q] = RecShape{0, 0, 0, 0};
+        srec[q] = RecShape{0, 0, 0, 0};
         if (r0 + q < count)
         {
-            sh_rec[q] = rec_shape(uint64_t(base) + off[r0 + q], len[r0 + q]);
-            rec_counts_add(sh_rec[q], c);
+            srec[q] = rec_shape(uint64_t(base) + off[r0 + q], len[r0 + q]);
+            tc.add_record(srec[q]);
         }
     }
     // block exclusive scan of the packed counts
     uint32_t p[kPacked], x[kPacked];
-    pack_counts(c, p);
+    pack_counts(tc, p);
 #pragma unroll
     for (int w = 0; w < kPacked; ++w)
     {
@@ -615,34 +633,41 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
     }
     __syncthreads();
     if (total_items > item_cap) return;  // host re-plans with a larger workspace
-    uint32_t pos[kBins];
-    unpack_counts(ex, pos);
+    // this thread's next free slot per bin, in LDS (bank = thread, whatever the bin)
+    {
+        uint32_t e[kBins];
+        unpack_counts(ex, e);
 #pragma unroll
-    for (uint32_t b = 0; b < kBins; ++b) pos[b] += bin_base[b];
+        for (uint32_t b = 0; b < kBins; ++b) slot[b][threadIdx.x] = bin_base[b] + e[b];
+    }
+    auto take = [&](uint32_t b, uint32_t n) {
+        const uint32_t v = slot[b][threadIdx.x];
+        slot[b][threadIdx.x] = v + n;
+        return v;
+    };
 
 #pragma unroll
     for (uint32_t q = 0; q < kPlanPer; ++q)
     {
-        const RecShape& s = sh_rec[q];
+        const RecShape& s = srec[q];
         const uint64_t r = r0 + q;
         uint32_t nint_w = 0, ip = 0;  // interior run this lane hands to its wave
         if (r < count && s.n != 0)
         {
             // bin 0 holds, in order: first (if bin 0), interior pieces, last (if bin 0)
-            const uint32_t fp = pos[piece_bin(s, 0)]++;
+            const uint32_t fp = take(piece_bin(s, 0), 1);
             items[fp] = piece_item(s, 0);
             first_pos[r] = fp;
             if (s.n >= 2)
             {
                 const uint32_t nint = s.n - 2;
-                ip = pos[0];
+                ip = take(0, nint);
                 int_pos[r] = ip;
                 if (nint > kLongChunks)
                     longs[atomicAdd(plan_hdr_d(blk, nblocks) + kHdrLongs, 1u)] = uint32_t(r);
                 else
                     nint_w = nint;
-                pos[0] += nint;
-                const uint32_t lp = pos[piece_bin(s, s.n - 1)]++;
+                const uint32_t lp = take(piece_bin(s, s.n - 1), 1);
                 items[lp] = piece_item(s, s.n - 1);
                 last_pos[r] = lp;
             }
@@ -653,10 +678,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
         {
             const int l = __builtin_ctzll(pending);
             pending &= pending - 1;
-            const uint32_t n_l = __shfl(nint_w, l);
-            const uint32_t ip_l = __shfl(ip, l);
-            const uint64_t k0_l = uint64_t(__shfl(uint32_t(s.k0), l)) |
-                                  (uint64_t(__shfl(uint32_t(s.k0 >> 32), l)) << 32);
+            // readlane returns int: go through uint32_t so the halves zero-extend
+            const uint32_t n_l = uint32_t(__builtin_amdgcn_readlane(int(nint_w), l));
+            const uint32_t ip_l = uint32_t(__builtin_amdgcn_readlane(int(ip), l));
+            const uint32_t k0_lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(s.k0)), l));
+            const uint32_t k0_hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(s.k0 >> 32)), l));
+            const uint64_t k0_l = uint64_t(k0_lo) | (uint64_t(k0_hi) << 32);
             for (uint32_t j = lane; j < n_l; j += 64) items[ip_l + j] = interior_item(k0_l, j);
         }
     }
@@ -915,16 +942,28 @@ __device__ __forceinline__ uint32_t zneg(const uint32_t* p2, const uint32_t* zin
     return m ? zglob(zinv, zbits(p2, v, kRowBytes - m)) : v;
 }
 
-// Register after a record's first piece when started from `x`.
+// Register after a record's first piece: the seed ~init shifted across the
+// piece's window, `sx` = Z_{w-a}(~init), XORed with R0 and the trailing m
+// zeros undone.  window [.., w), piece [a, pe), m = w - pe, R0 = Z_m(raw(piece)):
+// state = Z_{pe-a}(~init) ^ raw(piece) = Z_{-m}(sx ^ R0).
 __device__ __forceinline__ uint32_t first_piece_state(const RecShape& s, const uint32_t* p2,
-                                                      const uint32_t* zinv, uint32_t x,
+                                                      const uint32_t* zinv, uint32_t sx,
                                                       uint32_t R0)
 {
-    // window [.., w), piece [a, pe), m = w - pe: R0 = Z_m(raw(piece));
-    // state = Z_{pe-a}(x) ^ raw(piece) = Z_{-m}(Z_{w-a}(x) ^ R0)
     const uint64_t pe = piece_end(s, 0);
     const uint64_t w = (pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
-    return zneg(p2, zinv, zbits(p2, x, uint32_t(w - s.a)) ^ R0, uint32_t(w - pe));
+    return zneg(p2, zinv, sx ^ R0, uint32_t(w - pe));
+}
+
+// Z_{w-a}(~init) for the first piece (w - a <= 4096): with no inits, one
+// load from F = Z_n(~0) (issued before the partials arrive); else the shift.
+__device__ __forceinline__ uint32_t first_seed(const RecShape& s, const uint32_t* p2,
+                                               const uint32_t* __restrict__ finit,
+                                               const uint32_t* __restrict__ inits, uint64_t r)
+{
+    const uint64_t pe = piece_end(s, 0);
+    const uint32_t n = uint32_t(((pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1)) - s.a);
+    return inits ? zbits(p2, ~inits[r], n) : finit[n];
 }
 
 // Register after the last piece (n >= 2) from the state before it.
@@ -973,7 +1012,8 @@ __global__ __launch_bounds__(512) void crc32c_finalize_kernel(
         else
         {
             if (s.n >= 2 && s.n - 2 > kLongChunks) continue;  // long_finalize_kernel
-            c = first_piece_state(s, p2, zinv, c, partial[first_pos[r]]);
+            const uint32_t sx = first_seed(s, p2, tables + kTabFInit, inits, r);
+            c = first_piece_state(s, p2, zinv, sx, partial[first_pos[r]]);
             if (s.n >= 2)
             {
                 const uint32_t ip = int_pos[r];
@@ -1035,7 +1075,7 @@ __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
         {
             uint32_t c = 0;
             for (int w = 0; w < kLongBlock / 64; ++w) c ^= red[w];
-            uint32_t h = first_piece_state(s, p2, zinv, ~(inits ? inits[r] : 0u),
+            uint32_t h = first_piece_state(s, p2, zinv, first_seed(s, p2, tables + kTabFInit, inits, r),
                                            partial[first_pos[r]]);
             uint64_t n = uint64_t(nint) * kChunk;  // bytes of the interior run
             for (int b = 0; n && b < 48; ++b, n >>= 1)

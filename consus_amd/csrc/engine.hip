@@ -106,6 +106,16 @@ int init_device(int device)
         }
         make_op_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZInv128]), inv);
     }
+    {
+        // F[n] = Z_n(~0): the register a zero init reaches after n bytes of zeros
+        const uint32_t* t0 = &img[kTabT];
+        uint32_t f = 0xFFFFFFFFu;
+        for (int n = 0; n <= int(kChunk); ++n)
+        {
+            img[kTabFInit + n] = f;
+            f = t0[f & 0xFFu] ^ (f >> 8);
+        }
+    }
     std::vector<uint32_t> pow2(48 * 1024);
     Op32 p = Op32::zero_byte();
     for (int k = 0; k < 64; ++k)

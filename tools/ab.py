@@ -19,3 +19,7 @@ for rnd in range(3):
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
         line = (r.stdout.strip().splitlines() or ["<no output> " + r.stderr[-300:]])[-1]
         print(f"round {rnd} {os.path.basename(lib):28s} {line}", flush=True)
+        # a GPU fault or a wrong digest ends the session: nothing more runs on the GPU
+        if r.returncode != 0 or "HSA_STATUS_ERROR" in r.stdout + r.stderr or "MISMATCH" in line:
+            print(r.stderr[-2000:], file=sys.stderr)
+            sys.exit(1)
