@@ -545,9 +545,76 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
     }
 }
 
-// Each block finds its own base in every bin from the per-block counts (no
-// separate scan pass): wave b < kBins sums bin b over all blocks and over the
-// blocks before this one.  Block 0 publishes the plan header.
+// One workgroup turns the bin-major block counts into bases in place: the
+// exclusive scan of the flat array [bin][block] is exactly "items of earlier
+// bins + items of this bin in earlier blocks".  Tiles of 16K entries are
+// staged through LDS (loads and stores coalesced; index padded one word per
+// 32 against bank conflicts), each thread scans 16 consecutive entries.  The
+// header gets the bin starts and the item total.
+constexpr uint32_t kScanPer = 16;
+constexpr uint32_t kScanTile = 1024 * kScanPer;
+
+__device__ __forceinline__ uint32_t scan_slot(uint32_t i) { return i + (i >> 5); }
+
+__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ blk,
+                                                         uint32_t nblocks)
+{
+    __shared__ uint32_t tile[kScanTile + kScanTile / 32];
+    __shared__ uint32_t sh[16];
+    __shared__ uint32_t carry;
+    const uint32_t n = kBins * nblocks;
+    uint32_t* hdr = plan_hdr_d(blk, nblocks);
+    if (threadIdx.x == 0) carry = 0;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t base = 0; base < n; base += kScanTile)
+    {
+        const uint32_t cnt = min(kScanTile, n - base);
+        for (uint32_t i = threadIdx.x; i < kScanTile; i += 1024)
+            tile[scan_slot(i)] = i < cnt ? blk[base + i] : 0u;
+        __syncthreads();
+        uint32_t v[kScanPer], sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kScanPer; ++j)
+        {
+            v[j] = tile[scan_slot(threadIdx.x * kScanPer + j)];
+            sum += v[j];
+        }
+        uint32_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane >= uint32_t(d)) x += y;
+        }
+        if (lane == 63) sh[wave] = x;
+        __syncthreads();
+        uint32_t run = carry + x - sum, tot = 0;
+        for (uint32_t w = 0; w < 16; ++w)
+        {
+            if (w < wave) run += sh[w];
+            tot += sh[w];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kScanPer; ++j)
+        {
+            tile[scan_slot(threadIdx.x * kScanPer + j)] = run;
+            run += v[j];
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < cnt; i += 1024)
+        {
+            const uint32_t e = tile[scan_slot(i)];
+            blk[base + i] = e;
+            if ((base + i) % nblocks == 0) hdr[(base + i) / nblocks] = e;  // bin start
+        }
+        if (threadIdx.x == 0) carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) hdr[kHdrTotal] = carry;
+}
+
+// Each block reads its base in every bin (plan_scan_kernel) and hands its
+// threads their slots.
 __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, uint64_t count, uint32_t* __restrict__ blk,
@@ -555,31 +622,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
     uint32_t* __restrict__ first_pos, uint32_t* __restrict__ int_pos,
     uint32_t* __restrict__ last_pos, uint32_t* __restrict__ longs)
 {
-    __shared__ uint32_t tot[kBins], pre[kBins], bin_base[kBins];
-    __shared__ uint32_t total_items;
+    __shared__ uint32_t bin_base[kBins];
     __shared__ uint32_t slot[kBins][kPlanThreads];
     __shared__ uint32_t sh[kPlanThreads / 64][kPacked];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (wave < kBins)
-    {
-        uint32_t t = 0, before = 0;
-        for (uint32_t b = lane; b < nblocks; b += 64)
-        {
-            const uint32_t v = blk[wave * nblocks + b];
-            t += v;
-            before += b < blockIdx.x ? v : 0u;
-        }
-        for (int d = 32; d >= 1; d >>= 1)
-        {
-            t += __shfl_xor(t, d);
-            before += __shfl_xor(before, d);
-        }
-        if (lane == 0)
-        {
-            tot[wave] = t;
-            pre[wave] = before;
-        }
-    }
+    if (plan_hdr_d(blk, nblocks)[kHdrTotal] > item_cap) return;  // host re-plans (uniform)
+    if (threadIdx.x < kBins) bin_base[threadIdx.x] = blk[threadIdx.x * nblocks + blockIdx.x];
 
     // this thread's records and their counts (overlaps the loads above)
     const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kPlanPer;
@@ -611,18 +659,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
     if (lane == 63)
         for (int w = 0; w < kPacked; ++w) sh[wave][w] = x[w];
     __syncthreads();
-    if (threadIdx.x == 0)
-    {
-        uint32_t run = 0;
-        for (uint32_t b = 0; b < kBins; ++b)
-        {
-            bin_base[b] = run + pre[b];
-            if (blockIdx.x == 0) plan_hdr_d(blk, nblocks)[b] = run;
-            run += tot[b];
-        }
-        total_items = run;
-        if (blockIdx.x == 0) plan_hdr_d(blk, nblocks)[kHdrTotal] = run;
-    }
     uint32_t ex[kPacked];
 #pragma unroll
     for (int w = 0; w < kPacked; ++w)
@@ -631,8 +667,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
         for (uint32_t v = 0; v < wave; ++v) acc += sh[v][w];
         ex[w] = acc;
     }
-    __syncthreads();
-    if (total_items > item_cap) return;  // host re-plans with a larger workspace
     // this thread's next free slot per bin, in LDS (bank = thread, whatever the bin)
     {
         uint32_t e[kBins];
@@ -715,6 +749,7 @@ hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint
     const uint8_t* b = static_cast<const uint8_t*>(base);
     hipLaunchKernelGGL(plan_count_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, count, ws.blk, nb);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, nb);
     hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, count, ws.blk, nb, ws.items, ws.item_cap, ws.first_pos,
                        ws.int_pos, ws.last_pos, ws.longs);

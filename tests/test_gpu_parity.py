@@ -186,3 +186,25 @@ def test_rccl_single_rank_allgather(engine, oracle):
         assert np.array_equal(got, oracle.fixed(data.download(np.uint8), 256, 256, count))
     finally:
         engine.comm_destroy()
+
+
+def test_var_many_records_multi_tile_plan(engine, oracle):
+    """6.5M short records: > 1,587 plan blocks, so the bin scan runs over
+    several LDS tiles, and the scatter's per-block bases come from it."""
+    rng = np.random.default_rng(21)
+    count = 6_500_000
+    lengths = rng.integers(0, 97, count, dtype=np.uint32)
+    lengths[rng.integers(0, count, 64)] = 70_000            # a few multi-chunk records
+    offsets = np.zeros(count, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    total = int(lengths.sum(dtype=np.uint64))
+    data = engine.DeviceBuffer(total + 16)
+    data.fill_splitmix64(0x5CA1E)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=total)
+    got = d_out.download(np.uint32, count)
+    host = data.download(np.uint8, total)
+    assert np.array_equal(got, oracle.batch(host, offsets, lengths))
