@@ -34,7 +34,8 @@ constexpr int kTabP2 = kTabZC2 + 10 * 1024;    // G^{2^k}, k = 0..12 (shifts up 
 constexpr int kTabZInv128 = kTabP2 + 13 * 1024; // Z_{-128} = (Z_128)^{-1}
 constexpr int kTabZero = kTabZInv128 + 1024;    // 4 zero words (init 0 when inits == nullptr)
 constexpr int kTabFInit = kTabZero + 4;         // Z_n(0xFFFFFFFF), n = 0..4096 (init 0 seeds)
-constexpr int kTabWords = kTabFInit + 4097;
+constexpr int kTabZRows = kTabFInit + 4100;     // G^{128 k}, k = 1..32 (last-piece shifts)
+constexpr int kTabWords = kTabZRows + 32 * 1024;
 
 // LDS image of the record kernels (bytes).
 constexpr uint32_t kLdsMain = 0;            // 128 KiB bank-private G^{128}

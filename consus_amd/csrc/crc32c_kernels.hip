@@ -1001,14 +1001,18 @@ __device__ __forceinline__ uint32_t first_seed(const RecShape& s, const uint32_t
     return inits ? zbits(p2, ~inits[r], n) : finit[n];
 }
 
-// Register after the last piece (n >= 2) from the state before it.
+// Register after the last piece (n >= 2) from the state before it.  The
+// piece starts on a chunk boundary, so its window is 128 k bytes (k <= 32):
+// one G^{128 k} table set (global, L2-resident) instead of a bit-serial shift.
 __device__ __forceinline__ uint32_t last_piece_state(const RecShape& s, const uint32_t* p2,
-                                                     const uint32_t* zinv, uint32_t x,
-                                                     uint32_t R)
+                                                     const uint32_t* zinv,
+                                                     const uint32_t* __restrict__ zrows,
+                                                     uint32_t x, uint32_t R)
 {
     const uint64_t ps = piece_start(s, s.n - 1), pe = s.E;
     const uint64_t w = (pe + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
-    return zneg(p2, zinv, zbits(p2, x, uint32_t(w - ps)) ^ R, uint32_t(w - pe));
+    const uint32_t k = uint32_t(w - ps) / kRowBytes;
+    return zneg(p2, zinv, zglob(zrows + (k - 1) * 1024, x) ^ R, uint32_t(w - pe));
 }
 
 // One thread per record: Horner from ~init over its pieces (see the section
@@ -1023,14 +1027,14 @@ __global__ __launch_bounds__(512) void crc32c_finalize_kernel(
     __shared__ uint32_t t0[256];
     __shared__ uint32_t zc[1024];
     __shared__ uint32_t zinv[1024];
-    __shared__ uint32_t p2[13 * 1024];
+    __shared__ uint32_t p2[7 * 1024];  // G^{2^k}, k < 7: the Z_{128-m} of zneg
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) t0[i] = tables[kTabT + i];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x)
     {
         zc[i] = tables[kTabZChunk + i];
         zinv[i] = tables[kTabZInv128 + i];
     }
-    for (uint32_t i = threadIdx.x; i < 13 * 1024; i += blockDim.x) p2[i] = tables[kTabP2 + i];
+    for (uint32_t i = threadIdx.x; i < 7 * 1024; i += blockDim.x) p2[i] = tables[kTabP2 + i];
     __syncthreads();
     // persistent grid: the tables are staged once per workgroup
     for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < count;
@@ -1047,13 +1051,13 @@ __global__ __launch_bounds__(512) void crc32c_finalize_kernel(
         else
         {
             if (s.n >= 2 && s.n - 2 > kLongChunks) continue;  // long_finalize_kernel
-            const uint32_t sx = first_seed(s, p2, tables + kTabFInit, inits, r);
+            const uint32_t sx = first_seed(s, tables + kTabP2, tables + kTabFInit, inits, r);
             c = first_piece_state(s, p2, zinv, sx, partial[first_pos[r]]);
             if (s.n >= 2)
             {
                 const uint32_t ip = int_pos[r];
                 for (uint32_t j = 0; j + 2 < s.n; ++j) c = zglob(zc, c) ^ partial[ip + j];
-                c = last_piece_state(s, p2, zinv, c, partial[last_pos[r]]);
+                c = last_piece_state(s, p2, zinv, tables + kTabZRows, c, partial[last_pos[r]]);
             }
         }
         out[r] = ~c;
@@ -1116,7 +1120,7 @@ __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
             for (int b = 0; n && b < 48; ++b, n >>= 1)
                 if (n & 1u) h = zglob(pow2 + b * 1024, h);
             c ^= h;
-            out[r] = ~last_piece_state(s, p2, zinv, c, partial[last_pos[r]]);
+            out[r] = ~last_piece_state(s, p2, zinv, tables + kTabZRows, c, partial[last_pos[r]]);
         }
         __syncthreads();
     }
@@ -1129,9 +1133,9 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
 {
     if (count == 0) return hipSuccess;
     const uint8_t* b = static_cast<const uint8_t*>(base);
-    // two 512-thread workgroups per CU fit the 62 KB of tables each stages
+    // four 512-thread workgroups per CU fit the 37 KB of tables each stages
     const uint64_t fin_blocks = (count + 511) / 512;
-    hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(uint32_t(fin_blocks < 512 ? fin_blocks : 512)),
+    hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(uint32_t(fin_blocks < 1024 ? fin_blocks : 1024)),
                        dim3(512), 0,
                        stream, b, offsets, lengths, inits, count, ws.partial, ws.first_pos,
                        ws.int_pos, ws.last_pos, out, tables);

@@ -97,6 +97,9 @@ int init_device(int device)
     for (int b = 0; b < 13; ++b)
         make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabP2 + b * 1024]),
                          uint64_t(1) << b);
+    for (int k = 1; k <= 32; ++k)
+        make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZRows + (k - 1) * 1024]),
+                         uint64_t(kRowBytes) * k);
     {
         Op32 inv;
         if (!invert(zeros_op(kRowBytes), &inv))
