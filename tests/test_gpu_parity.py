@@ -208,3 +208,28 @@ def test_var_many_records_multi_tile_plan(engine, oracle):
     got = d_out.download(np.uint32, count)
     host = data.download(np.uint8, total)
     assert np.array_equal(got, oracle.batch(host, offsets, lengths))
+
+
+def test_var_alignment_sweep(engine, oracle):
+    """Every start residue mod 128 and starts just before 4 KiB boundaries,
+    with lengths at row (128 B), group (1 KiB) and chunk (4 KiB) edges, with
+    and without inits: the masking, bin and window-shift cases of the plan."""
+    rng = np.random.default_rng(22)
+    starts = list(range(0, 128)) + [4096 - d for d in (1, 2, 3, 4, 15, 16, 17, 127, 128, 129,
+                                                       1023, 1024, 1025)]
+    lens = [1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 127, 128, 129, 255, 256, 257, 511,
+            512, 513, 1023, 1024, 1025, 2047, 2048, 2049, 3071, 3072, 3073, 4095, 4096, 4097,
+            8191, 8192, 8193, 12289, 70000]
+    offsets, lengths = [], []
+    for i, s in enumerate(starts):
+        for j, n in enumerate(lens):
+            offsets.append(((i * len(lens) + j) * 3) * 4096 + 8192 + s)
+            lengths.append(n)
+    offsets = np.array(offsets, dtype=np.uint64)
+    lengths = np.array(lengths, dtype=np.uint32)
+    buf = rng.integers(0, 256, int((offsets + lengths).max()) + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
