@@ -58,10 +58,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="fixed4k", choices=["fixed4k", "zipf", "stream", "pcie4k"],
+    ap.add_argument("--config", default="fixed4k",
+                    choices=["fixed4k", "zipf", "stream", "pcie4k", "single"],
                     help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2]; "
                          "stream = configs[4] (64 MiB host segments, H2D+CRC+D2H); pcie4k = "
-                         "configs[1] bytes starting in pinned host memory")
+                         "configs[1] bytes starting in pinned host memory; single = the same "
+                         "4 GiB as ONE device-resident record (long-record path, SURVEY 8(f)4)")
     ap.add_argument("--segments", type=int, default=16, help="stream/pcie4k: segments per step")
     ap.add_argument("--records-per-rank", type=int, default=1 << 20)
     ap.add_argument("--record-bytes", type=int, default=RECORD)
@@ -240,6 +242,33 @@ def run_secondary(args, E) -> dict:
                          "kernel": "plan + crc32c_chunk_kernel + finalize (whole step)"},
             "digest_verified": (dig == g.get("digest")) if g and R == 1 << 20 else None,
             "digests": [f"{dig:#010x}"]})
+        return res
+    if args.config == "single":
+        n = 1 << 32
+        gs = gold.get("single_record_seed0xc0de", {}).get("crc", {})
+        data = E.DeviceBuffer(n + 4097)
+        data.fill_splitmix64(SEED)
+        for _ in range(args.warmup):
+            E.crc32c_device(data, n)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            got = E.crc32c_device(data, n)   # synchronous: plan, kernels, host combine
+        wall = (time.perf_counter() - t0) / args.steps
+        odd = E.crc32c_device(data, n + 4097)
+        ok = (got == gs.get(str(n)) and odd == gs.get(str(n + 4097))) if gs else None
+        res.update({
+            "metric": "GiB/s CRC32C of one device-resident 4 GiB record (consus::crc32c semantics)",
+            "value": round(n / wall / 2**30, 2), "unit": "GiB/s", "ms_per_step": round(wall * 1e3, 4),
+            "data": "synthetic: splitmix64 stream 0xC0DE in HBM (the cfg-2 bytes as one record)",
+            "config": {"workload": "1 x 4 GiB record, device-resident, 1 x MI355X; 16 MiB "
+                                   "pieces (4,096 chunks each, long-record path) joined on the "
+                                   "GPU by crc32c_chain_kernel"},
+            "roofline": {"bound": "hbm", "achieved": round(n / wall / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(n / wall / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "plan + crc32c_chunk_kernel<4> + long_finalize + chain "
+                                   "(whole call, host sync included)"},
+            "digest_verified": ok, "crc": f"{got:#010x}"})
         return res
     # stream / pcie4k: host-resident segments through the H2D -> CRC -> D2H pipeline
     nseg = args.segments

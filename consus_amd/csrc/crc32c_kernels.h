@@ -91,6 +91,8 @@ constexpr uint32_t kPlanHdrTotal = kBins;
 constexpr uint32_t kPlanHdrWords = kBins + 4;
 inline uint32_t* plan_hdr(uint32_t* blk, uint32_t nblocks) { return blk + kBins * nblocks; }
 
+hipError_t launch_chain(const uint32_t* crcs, const uint64_t* after, uint32_t np, uint32_t* out,
+                        const uint32_t* pow2_tables, hipStream_t stream);
 hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,
                           uint64_t count, uint32_t* out, const uint32_t* pow2_tables,
                           hipStream_t stream);

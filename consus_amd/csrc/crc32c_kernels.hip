@@ -1193,6 +1193,45 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(
     out[i] = s ^ b[i];
 }
 
+// One CRC from consecutive pieces: out = XOR_i Z_{after_i}(crc_i), after_i
+// = bytes of the pieces behind piece i (identity 1 of DESIGN.md section 3,
+// applied to every piece at once instead of a serial Horner chain).  One
+// workgroup; G^{2^k} tables from global memory.
+__global__ __launch_bounds__(1024) void crc32c_chain_kernel(const uint32_t* __restrict__ crcs,
+                                                            const uint64_t* __restrict__ after,
+                                                            uint32_t np, uint32_t* __restrict__ out,
+                                                            const uint32_t* __restrict__ pow2)
+{
+    __shared__ uint32_t red[16];
+    uint32_t acc = 0;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x)
+    {
+        uint32_t s = crcs[i];
+        uint64_t n = after[i];
+        for (int k = 0; n && k < 48; ++k, n >>= 1)
+            if (n & 1u) s = zglob(pow2 + k * 1024, s);
+        acc ^= s;
+    }
+    for (int d = 32; d >= 1; d >>= 1) acc ^= __shfl_xor(acc, d);
+    if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        uint32_t r = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; ++w) r ^= red[w];
+        out[0] = r;
+    }
+}
+
+hipError_t launch_chain(const uint32_t* crcs, const uint64_t* after, uint32_t np, uint32_t* out,
+                        const uint32_t* pow2_tables, hipStream_t stream)
+{
+    if (np == 0) return hipSuccess;
+    hipLaunchKernelGGL(crc32c_chain_kernel, dim3(1), dim3(1024), 0, stream, crcs, after, np, out,
+                       pow2_tables);
+    return hipGetLastError();
+}
+
 hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,
                           uint64_t count, uint32_t* out, const uint32_t* pow2_tables,
                           hipStream_t stream)

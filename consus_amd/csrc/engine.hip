@@ -452,36 +452,49 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
     Ctx* c = thread_ctx(&st);
     if (!c) return st;
     DeviceState* d = g_dev.load();
-    // Pieces of <= 1 GiB computed as one batch, chained with the combine
-    // identity crc(0, A||B) = Z_|B|(crc(0, A)) ^ crc(0, B); init goes into piece 0.
-    constexpr uint64_t kPiece = 1ull << 30;
+    // Pieces of <= 16 MiB computed as one batch (one long-path record each,
+    // so a 4 GiB buffer keeps 256 workgroups of long_finalize busy) and
+    // joined with the combine identity crc(0, A||B) = Z_|B|(crc(0, A)) ^
+    // crc(0, B); init goes into piece 0.
+    constexpr uint64_t kPiece = 16ull << 20;
     const size_t np = size_t((n + kPiece - 1) / kPiece);
-    std::vector<uint64_t> off(np);
+    if (np >= (1ull << 31)) return fail(MI_CRC32C_EINVAL, "buffer too large");
+    std::vector<uint64_t> off(np), after(np);
     std::vector<uint32_t> len(np), ini(np, 0), res(np);
     for (size_t i = 0; i < np; ++i)
     {
         off[i] = i * kPiece;
         len[i] = uint32_t(std::min<uint64_t>(kPiece, n - i * kPiece));
+        after[i] = n - off[i] - len[i];
     }
     ini[0] = init;
     if (flags & MI_CRC32C_DEVICE)
     {
+        DevBuf& d_after = c->data;  // device staging unused on the device path
         if ((st = c->off.reserve(np * 8)) || (st = c->len.reserve(np * 4)) ||
-            (st = c->inits.reserve(np * 4)) || (st = c->out.reserve(np * 4)))
+            (st = c->inits.reserve(np * 4)) || (st = c->out.reserve(np * 4 + 4)) ||
+            (st = d_after.reserve(np * 8)))
             return st;
         HIP_TRY(hipMemcpyAsync(c->off.p, off.data(), np * 8, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(c->len.p, len.data(), np * 4, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(c->inits.p, ini.data(), np * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(d_after.p, after.data(), np * 8, hipMemcpyHostToDevice, c->stream));
         if ((st = run_var(d, c, data, c->off.as<uint64_t>(), c->len.as<uint32_t>(),
                           c->inits.as<uint32_t>(), np, n, c->out.as<uint32_t>())))
             return st;
-        HIP_TRY(hipMemcpyAsync(res.data(), c->out.p, np * 4, hipMemcpyDeviceToHost, c->stream));
+        uint32_t* dres = c->out.as<uint32_t>() + np;
+        HIP_TRY(launch_chain(c->out.as<uint32_t>(), d_after.as<uint64_t>(), uint32_t(np), dres,
+                             d->d_pow2, c->stream));
+        uint32_t* h = c->pin_small.as<uint32_t>();
+        HIP_TRY(hipMemcpyAsync(h, dres, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        *out = *h;
+        return MI_CRC32C_OK;
     }
-    else if ((st = mi_crc32c_batch(data, off.data(), len.data(), ini.data(), np, n, res.data(), 0)))
+    if ((st = mi_crc32c_batch(data, off.data(), len.data(), ini.data(), np, n, res.data(), 0)))
         return st;
-    uint32_t acc = res[0];
-    for (size_t i = 1; i < np; ++i) acc = apply_zeros(d, acc, len[i]) ^ res[i];
+    uint32_t acc = 0;
+    for (size_t i = 0; i < np; ++i) acc ^= apply_zeros(d, res[i], after[i]);
     *out = acc;
     return MI_CRC32C_OK;
 }

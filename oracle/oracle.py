@@ -201,6 +201,12 @@ class Reference(_Lib):
                                      _ptr(ini, _u32p), off.size, _ptr(out, _u32p), threads)
         return out
 
+    def splitmix_stream(self, seed: int, byte_off: int, nbytes: int) -> int:
+        """consus::crc32c(0, stream bytes [byte_off, +nbytes)), chained in 4 MiB pieces."""
+        f = self.lib.ref_crc32c_splitmix_stream
+        f.restype, f.argtypes = C.c_uint32, [C.c_uint64, C.c_uint64, C.c_uint64]
+        return int(f(seed, byte_off, nbytes))
+
     def splitmix_fixed(self, seed: int, rec_len: int, first_rec: int, count: int,
                        threads: int = 8) -> np.ndarray:
         out = np.zeros(count, dtype=np.uint32)

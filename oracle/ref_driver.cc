@@ -112,6 +112,25 @@ REF_EXPORT void ref_crc32c_splitmix_fixed(uint64_t seed, size_t rec_len, uint64_
     });
 }
 
+// One CRC over bytes [byte_off, byte_off + nbytes) of the splitmix64 stream
+// `seed`, generated and hashed in 4 MiB pieces chained through init
+// (common/crc32c.cc:122-126: init is a previous CRC): the single-record
+// golden of bench.py --config single.
+REF_EXPORT uint32_t ref_crc32c_splitmix_stream(uint64_t seed, uint64_t byte_off, uint64_t nbytes)
+{
+    const size_t piece = size_t(4) << 20;
+    std::vector<unsigned char> buf(piece + 8);
+    uint32_t crc = 0;
+    for (uint64_t done = 0; done < nbytes;)
+    {
+        const size_t n = size_t(std::min<uint64_t>(piece, nbytes - done));
+        oracle_fill_stream(buf.data(), n, seed, byte_off + done);
+        crc = consus::crc32c(crc, buf.data(), n);
+        done += n;
+    }
+    return crc;
+}
+
 // Per-record CRCs of records [base_off + offsets[i], +lengths[i]) of the
 // splitmix64 stream `seed` (config 3: packed Zipf-length records), generated
 // on the fly per record.

@@ -185,6 +185,17 @@ def main() -> None:
                       "with config-3 entry lengths and stream 0xDA7A5EED entries, greedily packed "
                       "into 64 MiB segments; digest = crc32c(0, LE CRC vector) per segment",
         "segments": segs}
+    # one huge record (bench.py --config single): the whole
+    # first 4 GiB (and 4 GiB + 4097 B) of stream 0xC0DE as ONE crc32c
+    single = {}
+    for nbytes in (1 << 32, (1 << 32) + 4097):
+        single[str(nbytes)] = ref.splitmix_stream(0xC0DE, 0, nbytes)
+    digests["single_record_seed0xc0de"] = {
+        "definition": "crc32c(0, bytes [0, n) of the splitmix64 stream 0xC0DE) as one record, "
+                      "keyed by n", "crc": single,
+        "check_1MiB": ref.splitmix_stream(0xC0DE, 0, 1 << 20)}
+    assert digests["single_record_seed0xc0de"]["check_1MiB"] == \
+        orc.crc32c(0, orc.fill(1 << 20, 0xC0DE, 0))
     # durable-log framing example (txman/durable_log.cc:54-61, 215-224)
     hdr = (1).to_bytes(8, "big") + (5).to_bytes(8, "big")
     crc = ref.crc32c(ref.crc32c(0, hdr), b"hello")

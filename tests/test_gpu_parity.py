@@ -233,3 +233,18 @@ def test_var_alignment_sweep(engine, oracle):
                           oracle.batch(buf, offsets, lengths))
     assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits),
                           oracle.batch(buf, offsets, lengths, inits))
+
+
+def test_single_record_4GiB_golden(engine):
+    """One 4 GiB record (and 4 GiB + 4097 B) against the reference's own
+    chained crc32c over the same stream (tests/golden/digests.json)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")) as f:
+        gold = json.load(f)["single_record_seed0xc0de"]["crc"]
+    n = 1 << 32
+    data = engine.DeviceBuffer(n + 4097)
+    data.fill_splitmix64(0xC0DE)
+    assert engine.crc32c_device(data, n) == gold[str(n)]
+    assert engine.crc32c_device(data, n + 4097) == gold[str(n + 4097)]
+    data.free()
