@@ -97,6 +97,14 @@ hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const ui
                           uint64_t count, uint32_t* out, const uint32_t* pow2_tables,
                           hipStream_t stream);
 
+// One device buffer: head h bytes, m 4 KiB chunks (m + 2 <= 2^24), tail t;
+// crcs: m words, vals: kSingleVals words, out: 1 word (all device).
+constexpr uint32_t kSingleVals = 1026;
+hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, uint32_t init,
+                         uint32_t crc0, uint32_t* crcs, uint32_t* vals, uint32_t* out,
+                         const uint32_t* tables, const uint32_t* pow2, int grid,
+                         hipStream_t stream);
+
 hipError_t launch_make_fixed_records(uint64_t* off, uint32_t* len, uint64_t count, uint64_t stride,
                                      uint32_t length, hipStream_t stream);
 

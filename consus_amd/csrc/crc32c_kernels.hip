@@ -914,44 +914,64 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
     }
 }
 
-// One launch per bin (G = 4, 3, 2, 1): each specialisation alone fits the
-// 128-VGPR budget of a 16-wave workgroup; inlined together they spill.
-template <int G>
+// All bins in one launch with wave roles.  Measured on config 3 (MI355X):
+// the 4-group pieces are HBM-bound and reach the same rate with 4 waves per
+// CU as with 16, while the short pieces are bound by per-item latency and
+// want as many waves as possible; run one after the other they cost the sum
+// of the two, run side by side on every CU (4 "lead" waves on the 4-group
+// pieces, 12 on the rest) they overlap.  A batch with only one kind gives
+// every wave to it.  Item assignment is static: a global work queue would
+// need one atomic per grab on a single address, which serialised
+// (~12 ns/atomic chip-wide) into a 2x slower step when tried.
+constexpr uint32_t kLeadWaves = 4;
+constexpr uint32_t kLeadAuto = ~0u;  // lead_override: pick from the plan (any value > 16)
+
 __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
     const Item* __restrict__ items, const uint32_t* __restrict__ blk, uint32_t nblocks,
-    uint32_t* __restrict__ partial, uint64_t item_cap, const uint32_t* __restrict__ tables)
+    uint32_t* __restrict__ partial, uint64_t item_cap, const uint32_t* __restrict__ tables,
+    uint32_t lead_override)
 {
     const uint32_t* hdr = blk + kBins * nblocks;  // plan_hdr
     const uint32_t n_items = hdr[kHdrTotal];
-    if (n_items > item_cap) return;
-    // bin b = 4 - G is [hdr[b], hdr[b + 1]); G = 1 takes bins 3..10 (one
-    // group, 8..1 rows) as one range
-    const uint32_t b = 4 - G;
-    const uint32_t lo = hdr[b];
-    const uint32_t hi = b == 3 ? n_items : hdr[b + 1];
-    const uint32_t team = (blockIdx.x * kBlock + threadIdx.x) / kTeam;
-    const uint32_t nteams = gridDim.x * kBlock / kTeam;
-    if (hi <= lo || lo + (blockIdx.x * kBlock) / kTeam >= hi) return;  // whole workgroup idle
+    if (n_items > item_cap || n_items == 0) return;
+    // bins: [hdr[0], hdr[1]) 4 groups, [hdr[1], hdr[2]) 3, [hdr[2], hdr[3]) 2,
+    // [hdr[3], n_items) one group of 8..1 rows
+    const uint32_t b0 = hdr[0], b1 = hdr[1], b2 = hdr[2], b3 = hdr[3];
+    const uint32_t lead = lead_override <= 16 ? lead_override
+                          : b1 == b0          ? 0u
+                          : n_items == b1     ? 16u
+                                              : kLeadWaves;
     stage_tables(tables);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
     const uint32_t tl = threadIdx.x & (kTeam - 1);
-    chunk_bin<G>(items, lo, hi, partial, team, team & ~7u, nteams, tl, lane_info(),
-                 reinterpret_cast<const uint8_t*>(tables + kTabZero));
+    const uint32_t tw = (threadIdx.x & 63u) / kTeam;
+    const uint32_t li = lane_info();
+    const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
+    if (wave < lead)
+    {
+        const uint32_t team = (blockIdx.x * lead + wave) * kTeam + tw;
+        const uint32_t nteams = gridDim.x * lead * kTeam;
+        chunk_bin<4>(items, b0, b1, partial, team, team & ~7u, nteams, tl, li, zero16);
+    }
+    else
+    {
+        const uint32_t rest = 16u - lead;
+        const uint32_t team = (blockIdx.x * rest + (wave - lead)) * kTeam + tw;
+        const uint32_t nteams = gridDim.x * rest * kTeam;
+        chunk_bin<3>(items, b1, b2, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin<2>(items, b2, b3, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin<1>(items, b3, n_items, partial, team, team & ~7u, nteams, tl, li, zero16);
+    }
 }
 
 hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
                              const uint32_t* tables, int grid, hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
-    const uint32_t nb = var_plan_blocks(count);
     (void)inits;  // applied by the finalize kernels
-#define MI_LAUNCH_CHUNK(GG)                                                                      \
-    hipLaunchKernelGGL(crc32c_chunk_kernel<GG>, dim3(grid), dim3(kBlock), kLdsBytes, stream,    \
-                       ws.items, ws.blk, nb, ws.partial, ws.item_cap, tables)
-    MI_LAUNCH_CHUNK(4);
-    MI_LAUNCH_CHUNK(3);
-    MI_LAUNCH_CHUNK(2);
-    MI_LAUNCH_CHUNK(1);
-#undef MI_LAUNCH_CHUNK
+    hipLaunchKernelGGL(crc32c_chunk_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream, ws.items,
+                       ws.blk, var_plan_blocks(count), ws.partial, ws.item_cap, tables,
+                       kLeadAuto);
     return hipGetLastError();
 }
 
@@ -1242,6 +1262,177 @@ hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const ui
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// One large device buffer (consus::crc32c(init, data, n), common/crc32c.cc:
+// 122-126, on a device pointer).  The buffer [a, a + n) is cut as
+//   head      [a, E)            4 <= h = E - a < 4100 bytes, E 4 KiB-aligned
+//   interior  m chunks of 4 KiB from E (crc32c_fixed_pipe_kernel, init 0)
+//   tail      t < 4096 bytes
+// and joined with raw-register algebra:
+//   raw(chunk j) = crc_j ^ crc0,  crc0 = crc32c(0, 4096 zero bytes)
+//   s = raw(head window, ~init XORed into bytes a..a+3)
+//   s = Z_{4096 m}(s) ^ raw(interior);  s = Z_t(s) ^ raw(tail);  crc = ~s
+// raw(interior) is a two-level tree: single_tree_kernel folds S = 1024 R
+// consecutive chunk CRCs per workgroup (strided Horner over R per thread, then a
+// 1024-leaf tree of 4 KiB leaves, thread t taking chunks t + 1024 r);
+// single_join_kernel
+// (one workgroup) trees the per-workgroup values the same way and adds head
+// and tail, each hashed by the whole workgroup from a zero-masked window.
+// The chunk index space is padded with zero chunks at the FRONT (leading
+// zeros are free), so every tree is full.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSingleStaged = 36;  // G^{2^k}, k < 36, staged by single_join_kernel
+
+// Tree of the 1024 values of a workgroup: leaf i spans `unit` bytes (unit =
+// 2^k0); returns the raw register of the concatenation in thread 0.  `zt(l, v)`
+// applies Z_{unit 2^l}.
+template <typename ZT>
+__device__ __forceinline__ uint32_t block_tree(uint32_t x, ZT zt, uint32_t* sh)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int l = 0; l < 6; ++l) x = zt(l, x) ^ __shfl_xor(x, 1 << l);
+    if (lane == 0) sh[wave] = x;
+    __syncthreads();
+    if (wave == 0)
+    {
+        x = lane < 16 ? sh[lane] : 0u;
+#pragma unroll
+        for (int l = 6; l < 10; ++l) x = zt(l, x) ^ __shfl_xor(x, 1 << (l - 6));
+    }
+    return x;
+}
+
+// Raw register of the window [w, w + 1024 * B) of bytes, B = 4 or 8 per thread,
+// keeping only bytes in [lo, hi) (others read as zero, none is loaded) and
+// XORing `x4` (little-endian) into bytes [x_at, x_at + 4).  T = T_0..T_15
+// (global); p2[l] = G^{B 2^l} (LDS), l < 10.
+template <int B>
+__device__ __forceinline__ uint32_t window_raw(uint64_t w, uint64_t lo, uint64_t hi, uint64_t x_at,
+                                               uint32_t x4, const uint32_t* __restrict__ T,
+                                               const uint32_t (*p2)[1024], uint32_t* sh)
+{
+    const uint64_t p = w + uint64_t(threadIdx.x) * B;
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < B; ++i)
+    {
+        const uint64_t q = p + i;
+        uint32_t byte = (q >= lo && q < hi) ? *reinterpret_cast<const uint8_t*>(q) : 0u;
+        if (q >= x_at && q < x_at + 4) byte ^= (x4 >> (8 * (q - x_at))) & 0xFFu;
+        r ^= T[(B - 1 - i) * 256 + byte];  // byte i is followed by B - 1 - i bytes
+    }
+    return block_tree(r, [&](int l, uint32_t v) { return zglob(p2[l], v); }, sh);
+}
+
+// Workgroups [0, nblocks): the interior tree.  Workgroup nblocks: the head
+// (the 8 KiB window ending at E = a + h, ~init in the record's first 4
+// bytes); nblocks + 1: the tail (the 4 KiB window ending at the buffer end).
+// Results: vals[0, nblocks), vals[1024] = head, vals[1025] = tail.
+__global__ __launch_bounds__(1024) void single_tree_kernel(
+    const uint32_t* __restrict__ crcs, uint64_t pad, uint32_t crc0, uint32_t log_r,
+    uint64_t a, uint64_t h, uint64_t m, uint32_t t, uint32_t init,
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2,
+    uint32_t* __restrict__ vals)
+{
+    __shared__ uint32_t tab[11][1024];
+    __shared__ uint32_t sh[16];
+    const uint32_t nblocks = gridDim.x - 2;
+    if (blockIdx.x >= nblocks)
+    {
+        const bool head = blockIdx.x == nblocks;
+        const int k0 = head ? 3 : 2;  // G^{8 2^l} / G^{4 2^l}
+        for (uint32_t i = threadIdx.x; i < 10 * 1024; i += 1024)
+            tab[i >> 10][i & 1023] = pow2[k0 * 1024 + i];
+        __syncthreads();
+        const uint64_t E = a + h, b = E + m * kChunk;
+        const uint32_t* T = tables + kTabT;
+        uint32_t x = 0;
+        if (head)
+            x = window_raw<8>(E - 8192, a, E, a, ~init, T, tab, sh);
+        else if (t)
+            x = window_raw<4>(b + t - 4096, b, b + t, 0, 0, T, tab, sh);
+        if (threadIdx.x == 0) vals[head ? 1024 : 1025] = x;
+        return;
+    }
+    // tab[0] = Z_{4096 * 1024}, the thread's stride; tab[1 + l] = Z_{4096 * 2^l}
+    for (uint32_t i = threadIdx.x; i < 1024; i += 1024) tab[0][i] = pow2[22 * 1024 + i];
+    for (uint32_t i = threadIdx.x; i < 10 * 1024; i += 1024)
+        tab[1 + (i >> 10)][i & 1023] = pow2[12 * 1024 + i];
+    // thread t takes virtual chunks b S + t + 1024 r (coalesced); chunk v < pad is zero.
+    // Its Horner value H_t (stride Z_{4096 * 1024}) enters the span's raw register
+    // as Z_{4096 (1023 - t)}(H_t): a 1024-leaf tree of 4 KiB leaves.
+    const uint32_t R = 1u << log_r;
+    const uint64_t v0 = uint64_t(blockIdx.x) * (1024u << log_r) + threadIdx.x;
+    uint32_t v[16];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r)
+    {
+        const uint64_t c = v0 + uint64_t(r) * 1024;
+        v[r] = (r < R && c >= pad) ? crcs[c - pad] ^ crc0 : 0u;
+    }
+    __syncthreads();
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r)
+        if (r < R) acc = zglob(tab[0], acc) ^ v[r];
+    acc = block_tree(acc, [&](int l, uint32_t x) { return zglob(tab[1 + l], x); }, sh);
+    if (threadIdx.x == 0) vals[blockIdx.x] = acc;
+}
+
+// One workgroup: tree of the interior workgroups' values (leaf i =
+// workgroup i - (1024 - nblocks)), then s = Z_t(Z_{4096 m}(head) ^ interior)
+// ^ tail and crc = ~s.  G^{2^k}, k < kSingleStaged, staged in LDS.
+__global__ __launch_bounds__(1024) void single_join_kernel(uint64_t m, uint32_t t,
+                                                          uint32_t nblocks, uint32_t log_s,
+                                                          const uint32_t* __restrict__ vals,
+                                                          const uint32_t* __restrict__ pow2,
+                                                          uint32_t* __restrict__ out)
+{
+    extern __shared__ uint32_t p2s[];  // kSingleStaged x 1024
+    __shared__ uint32_t sh[16];
+    uint32_t(*p2)[1024] = reinterpret_cast<uint32_t(*)[1024]>(p2s);
+    for (uint32_t i = threadIdx.x; i < kSingleStaged * 1024; i += 1024) p2s[i] = pow2[i];
+    const uint32_t bv = threadIdx.x >= 1024 - nblocks ? vals[threadIdx.x - (1024 - nblocks)] : 0u;
+    __syncthreads();
+    const uint32_t xi = block_tree(bv, [&](int l, uint32_t v) { return zglob(p2[log_s + l], v); }, sh);
+    if (threadIdx.x == 0)
+    {
+        uint32_t s = vals[1024];
+        for (int k = 0; k < int(kSingleStaged) - 12; ++k)
+            if ((m >> k) & 1u) s = zglob(p2[12 + k], s);
+        s ^= xi;
+        for (int k = 0; k < 12; ++k)
+            if ((t >> k) & 1u) s = zglob(p2[k], s);
+        out[0] = ~(s ^ vals[1025]);
+    }
+}
+
+hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, uint32_t init,
+                         uint32_t crc0, uint32_t* crcs, uint32_t* vals, uint32_t* out,
+                         const uint32_t* tables, const uint32_t* pow2, int grid,
+                         hipStream_t stream)
+{
+    // S = 1024 R chunks per tree workgroup: about 128 workgroups (each stages
+    // 44 KB of tables, so fewer is cheaper) up to R = 16, then up to 1024
+    uint32_t log_r = 0;
+    while (log_r < 4 && (uint64_t(128) << (10 + log_r)) < m + 2) ++log_r;
+    const uint64_t S = uint64_t(1024) << log_r;
+    const uint64_t M = (m + 2 + S - 1) / S * S;  // leading chunks [0, M - m) are zero
+    const uint32_t nblocks = uint32_t(M / S);
+    // the join's top tree level G^{4096 S 2^9} must be staged; Z_{4096 m} needs m < 2^24
+    if (m == 0 || nblocks > 1024 || 22 + log_r + 9 >= kSingleStaged || (m >> 24) != 0)
+        return hipErrorInvalidValue;
+    const uint8_t* base = static_cast<const uint8_t*>(data) + h;
+    const hipError_t e = launch_fixed(base, kChunk, kChunk, nullptr, m, crcs, tables, grid, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(single_tree_kernel, dim3(nblocks + 2), dim3(1024), 0, stream, crcs, M - m,
+                       crc0, log_r, uint64_t(data), h, m, t, init, tables, pow2, vals);
+    hipLaunchKernelGGL(single_join_kernel, dim3(1), dim3(1024), kSingleStaged * 4096, stream, m,
+                       t, nblocks, 22 + log_r, vals, pow2, out);
+    return hipGetLastError();
+}
+
 // Allow the 152 KiB dynamic LDS image on the two persistent kernels.
 hipError_t configure_kernels()
 {
@@ -1257,13 +1448,12 @@ hipError_t configure_kernels()
     for (const void* f : k)
         if (e == hipSuccess)
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    const void* c[] = {reinterpret_cast<const void*>(&crc32c_chunk_kernel<4>),
-                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<3>),
-                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<2>),
-                       reinterpret_cast<const void*>(&crc32c_chunk_kernel<1>)};
-    for (const void* f : c)
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_chunk_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);
     return e;
 }
 

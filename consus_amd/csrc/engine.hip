@@ -45,6 +45,10 @@ int fail(int status, const std::string& msg)
             return fail(MI_CRC32C_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// Device buffers from this size take launch_single (fixed-record kernel on
+// the 4 KiB chunks + a two-level combine tree) instead of the variable path.
+constexpr uint64_t kSingleMin = 64 * 1024;
+
 struct DeviceState
 {
     int ordinal = -1;
@@ -52,6 +56,7 @@ struct DeviceState
     uint32_t* d_tables = nullptr;  // kTabWords
     uint32_t* d_pow2 = nullptr;    // 48 x 1024: G^{2^k}
     Op32 pow2_ops[64];             // host copies for mi_crc32c_combine
+    uint32_t crc0 = 0;             // crc32c(0, 4096 zero bytes): chunk CRC -> raw register
     std::string arch;
 };
 
@@ -119,6 +124,7 @@ int init_device(int device)
             f = t0[f & 0xFFu] ^ (f >> 8);
         }
     }
+    d->crc0 = ~img[kTabFInit + kChunk];
     std::vector<uint32_t> pow2(48 * 1024);
     Op32 p = Op32::zero_byte();
     for (int k = 0; k < 64; ++k)
@@ -452,7 +458,8 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
     Ctx* c = thread_ctx(&st);
     if (!c) return st;
     DeviceState* d = g_dev.load();
-    // Pieces of <= 16 MiB computed as one batch (one long-path record each,
+    // Device buffers of >= kSingleMin bytes (up to 64 GiB): launch_single.
+    // Otherwise pieces of <= 16 MiB computed as one batch (one long-path record each,
     // so a 4 GiB buffer keeps 256 workgroups of long_finalize busy) and
     // joined with the combine identity crc(0, A||B) = Z_|B|(crc(0, A)) ^
     // crc(0, B); init goes into piece 0.
@@ -468,6 +475,28 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
         after[i] = n - off[i] - len[i];
     }
     ini[0] = init;
+    if ((flags & MI_CRC32C_DEVICE) && n >= kSingleMin)
+    {
+        // head up to the next 4 KiB boundary (>= 4 bytes, so ~init lands in
+        // it), 4 KiB chunks through the fixed-record kernel, tail < 4 KiB
+        uint64_t h = (kChunk - uintptr_t(data) % kChunk) % kChunk;
+        if (h < 4) h += kChunk;
+        const uint64_t m = (n - h) / kChunk;
+        const uint32_t t = uint32_t(n - h - m * kChunk);
+        if (m + 2 <= (1ull << 24) - (1ull << 14))  // launch_single's limits
+        {
+            if ((st = c->out.reserve((m + kSingleVals + 1) * 4))) return st;
+            uint32_t* crcs = c->out.as<uint32_t>();
+            uint32_t* dres = crcs + m + kSingleVals;
+            HIP_TRY(launch_single(data, h, m, t, init, d->crc0, crcs, crcs + m, dres,
+                                  d->d_tables, d->d_pow2, d->cus, c->stream));
+            uint32_t* hr = c->pin_small.as<uint32_t>();
+            HIP_TRY(hipMemcpyAsync(hr, dres, 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            *out = *hr;
+            return MI_CRC32C_OK;
+        }
+    }
     if (flags & MI_CRC32C_DEVICE)
     {
         DevBuf& d_after = c->data;  // device staging unused on the device path

@@ -248,3 +248,32 @@ def test_single_record_4GiB_golden(engine):
     assert engine.crc32c_device(data, n) == gold[str(n)]
     assert engine.crc32c_device(data, n + 4097) == gold[str(n + 4097)]
     data.free()
+
+
+def test_device_single_buffer_sweep(engine, oracle):
+    """Device buffers of >= 64 KiB take launch_single (head up to the next
+    4 KiB boundary, 4 KiB chunks through the fixed-record kernel, tail, and a
+    two-level combine tree).  Starts at every head case (0-3 bytes before a
+    boundary push the head past it so ~init lands in the head), tails of 0,
+    1 and 4095 bytes, sizes around the 64 KiB threshold and multi-workgroup
+    trees, with and without inits."""
+    rng = np.random.default_rng(23)
+    total = (9 << 20) + 3 * 4096
+    data = engine.DeviceBuffer(total)
+    data.fill_splitmix64(0x51C6E)
+    host = data.download(np.uint8, total)
+    base_mod = data.ptr % 4096
+    cases = []
+    for start in (0, 1, 2, 3, 4, 5, 16, 127, 2048, 4091, 4092, 4093, 4094, 4095):
+        off = (start - base_mod) % 4096 + 4096
+        h = (4096 - (data.ptr + off) % 4096) % 4096
+        h = h + 4096 if h < 4 else h
+        for n in (65535, 65536, 65537, h + 16 * 4096, h + 16 * 4096 + 1, h + 16 * 4096 + 4095,
+                  (1 << 20) + 7, (4 << 20) + h, (8 << 20) + 12345):
+            cases.append((off, n))
+    for off, n in cases:
+        for init in (0, int(rng.integers(0, 2**32))):
+            assert off + n <= total
+            got = engine.crc32c_device(data, n, init_crc=init, offset=off)
+            assert got == oracle.crc32c(init, host, n, off), (off, n, init)
+    data.free()
