@@ -65,7 +65,9 @@ def parse():
                          "configs[1] bytes starting in pinned host memory; single = the same "
                          "4 GiB as ONE device-resident record (long-record path, SURVEY 8(f)4)")
     ap.add_argument("--segments", type=int, default=16, help="stream/pcie4k: segments per step")
-    ap.add_argument("--records-per-rank", type=int, default=1 << 20)
+    ap.add_argument("--records-per-rank", type=int, default=None,
+                    help="default: 1M (configs[1]) on one GPU, 2M per GPU when N > 1, so that "
+                         "N = 8 is configs[3] (16M x 4 KiB across 8 GPUs)")
     ap.add_argument("--record-bytes", type=int, default=RECORD)
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="wall budget of each CPU-baseline leg (single, all-threads)")
@@ -90,13 +92,16 @@ def golden_digests():
 # ---- HBM traffic from a separate rocprofv3 --pmc pass ---------------------------
 def pmc_traffic(args) -> tuple[float | None, str]:
     """Run this script under `rocprofv3 --pmc FETCH_SIZE` (its own pass, no
-    tracing domains) and return corrected HBM read bytes per launch."""
+    tracing domains) and return corrected HBM read bytes per launch of the
+    fixed kernel (fixed4k) or per step of the variable path (zipf: every
+    plan, chunk and finalize dispatch of one step)."""
     exe = shutil.which("rocprofv3")
     if not exe:
         return None, "rocprofv3 not found"
     out = tempfile.mkdtemp(prefix="pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc",
            "--", sys.executable, os.path.abspath(__file__), "--child-pmc",
+           "--config", args.config,
            "--records-per-rank", str(args.records_per_rank),
            "--record-bytes", str(args.record_bytes)]
     try:
@@ -104,19 +109,31 @@ def pmc_traffic(args) -> tuple[float | None, str]:
                        stderr=subprocess.DEVNULL, cwd=out)
     except Exception as e:  # noqa: BLE001 -- traffic is optional, the bench is not
         return None, f"rocprofv3 pass failed: {e}"
+    fixed = args.config == "fixed4k"
+    step_kernels = ("plan_", "long_items", "crc32c_chunk_kernel", "crc32c_finalize", "long_finalize")
     vals = []
     for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if KERNEL_MATCH in row.get("Kernel_Name", "") and \
-                        row.get("Counter_Name") == "FETCH_SIZE":
+                name = row.get("Kernel_Name", "")
+                if row.get("Counter_Name") != "FETCH_SIZE":
+                    continue
+                if (fixed and KERNEL_MATCH in name) or \
+                        (not fixed and any(k in name for k in step_kernels)):
                     vals.append(float(row["Counter_Value"]))
     shutil.rmtree(out, ignore_errors=True)
     if not vals:
         return None, "no FETCH_SIZE rows for the kernel"
     # FETCH_SIZE is in KiB; gfx950 tallies 128-B requests of wide streaming
     # reads at 64 B, so double it (MI355X_MICROARCH.md, HBM).
-    return 2.0 * 1024.0 * float(np.median(vals)), f"{len(vals)} dispatches, median, x2 gfx950 correction"
+    if fixed:
+        return 2.0 * 1024.0 * float(np.median(vals)), \
+            f"{len(vals)} dispatches, median, x2 gfx950 correction"
+    return 2.0 * 1024.0 * sum(vals) / PMC_CHILD_STEPS, \
+        f"sum over the step's dispatches / {PMC_CHILD_STEPS} steps, x2 gfx950 correction"
+
+
+PMC_CHILD_STEPS = 3
 
 
 # ---- N > 1: the optional RCCL gather (BASELINE configs[3]) -----
@@ -203,7 +220,7 @@ def cpu_baseline(args) -> dict:
             "first_crc": int(crc_ref[0])}
 
 
-def run_secondary(args, E) -> dict:
+def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
     """Configs 3 and 5 and the host-inclusive rate of config 2 (one GPU)."""
     from consus_amd import workload as W
     gold = golden_digests()
@@ -217,6 +234,10 @@ def run_secondary(args, E) -> dict:
         d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer(R * 4)
         d_off.upload(off)
         d_len.upload(ln)
+        if args.child_pmc:
+            for _ in range(PMC_CHILD_STEPS):
+                E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
+            return {}
         for _ in range(args.warmup):
             E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
         E.sync()
@@ -238,7 +259,9 @@ def run_secondary(args, E) -> dict:
                                    f"(BASELINE.json configs[2])", "total_bytes": total},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "step_ms_events": round(ev, 4),
+                         "traffic": None if traffic[0] is None else round(traffic[0]),
+                         "traffic_note": traffic[1], "algorithmic_bytes": total,
+                         "step_ms_events": round(ev, 4),
                          "kernel": "plan + crc32c_chunk_kernel + finalize (whole step)"},
             "digest_verified": (dig == g.get("digest")) if g and R == 1 << 20 else None,
             "digests": [f"{dig:#010x}"]})
@@ -356,11 +379,13 @@ def main():
     if world != args.gpus and not args.child_pmc:
         if world == 1 and args.gpus > 1:
             sys.exit("for --gpus N>1 launch with torch.distributed.run (one process per GPU)")
+    if args.records_per_rank is None:
+        args.records_per_rank = (2 << 20) if world > 1 and args.config == "fixed4k" else 1 << 20
 
     # Traffic pass first, before this process touches the GPU.
     traffic, traffic_note = (None, "skipped")
     if rank == 0 and world == 1 and not args.child_pmc and not args.no_pmc and \
-            args.config == "fixed4k":
+            args.config in ("fixed4k", "zipf"):
         traffic, traffic_note = pmc_traffic(args)
 
     # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.
@@ -370,7 +395,9 @@ def main():
     if args.config != "fixed4k":
         if world != 1:
             sys.exit("secondary configs run on one GPU")
-        print(json.dumps(run_secondary(args, E)), flush=True)
+        res = run_secondary(args, E, (traffic, traffic_note))
+        if not args.child_pmc:
+            print(json.dumps(res), flush=True)
         return
 
     dist = None
@@ -453,7 +480,8 @@ def main():
 
     total_bytes = world * R * L * args.steps
     value = total_bytes / wall / 2**30
-    per_launch_ms = ev_ms / args.steps
+    # per-GPU kernel rate; at N > 1 from the slowest rank's launches
+    per_launch_ms = ev_ms_max / args.steps
     achieved = R * L / (per_launch_ms * 1e-3) / 1e9
     rec = {
         "metric": METRIC,
@@ -470,8 +498,10 @@ def main():
         "data": "synthetic: splitmix64(0xC0DE ^ word) stream, generated in HBM before timing "
                 "(SURVEY.md 8(d))",
         "config": {
-            "workload": f"{R} x {L} B records, device-resident, {world} x MI355X "
-                        f"(BASELINE.json configs[1] per GPU)",
+            "workload": f"{R} x {L} B records per GPU, device-resident, {world} x MI355X "
+                        + ("(BASELINE.json configs[1])" if world == 1 else
+                           "(BASELINE.json configs[3] at N = 8: 16M x 4 KiB records)"
+                           if world * R == 16 << 20 else "(configs[3] shape)"),
             "records_per_rank": R, "record_bytes": L, "global_batch": world * R,
             "parallelism": f"record shards x{world}, no collective in the timed region",
         },
@@ -491,7 +521,7 @@ def main():
     else:
         rec["cpu_baseline"] = None
     if world > 1:
-        rec["roofline"]["launch_ms_max_over_ranks"] = round(ev_ms_max / args.steps, 4)
+        rec["roofline"]["launch_ms_rank0"] = round(ev_ms / args.steps, 4)
         rec["gather"] = rccl_gather(E, dist, rank, world, out, R, digests, rec) \
             if do_gather else None
     print(json.dumps(rec), flush=True)

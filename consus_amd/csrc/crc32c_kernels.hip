@@ -30,6 +30,7 @@
 #define MI_CRC_ABLATE 0
 #endif
 
+
 namespace mi_crc {
 
 extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -318,6 +319,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_pipe_kernel(
             // Keep all 8 loads ahead of this group's folding (the scheduler
             // would otherwise sink them into it to save registers).
             __builtin_amdgcn_sched_barrier(0);
+
             if (g == 0) cur[0].x ^= tl == 0 ? ~init_word : 0u;
 #pragma unroll
             for (int r = 0; r < kGroupRows; ++r) row_update(V, cur[r], li);
@@ -393,7 +395,10 @@ hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const u
 // counts live in blk[bin * nblocks + block]; the plan header follows them
 // (plan_hdr): bin starts [0, kBins), total items, long-record count.
 constexpr uint32_t kPlanThreads = 1024;
-constexpr uint32_t kPlanPer = 4;
+#ifndef MI_PLAN_PER
+#define MI_PLAN_PER 4
+#endif
+constexpr uint32_t kPlanPer = MI_PLAN_PER;
 constexpr uint32_t kPlanRecs = kPlanThreads * kPlanPer;
 constexpr uint32_t kHdrTotal = kPlanHdrTotal;
 constexpr uint32_t kHdrLongs = kBins + 1;

@@ -95,6 +95,92 @@ __global__ __launch_bounds__(1024, 1) void probe_teamN(const uint8_t* __restrict
     if (acc == 0x12345678u) sink[threadIdx.x] = acc;
 }
 
+
+// The team pattern with each cache-policy flag set on the 16-B loads (inline
+// asm: the compiler does not track these loads, so an explicit vmcnt(0)
+// precedes the use).
+#define MI_PROBE_POLICY(NAME, FLAGS)                                                             \
+    __global__ __launch_bounds__(1024, 1) void NAME(const uint8_t* __restrict__ base,            \
+                                                    uint64_t count, uint32_t* __restrict__ sink) \
+    {                                                                                            \
+        const uint32_t tl = threadIdx.x & 7;                                                     \
+        const uint64_t team = (uint64_t(blockIdx.x) * 1024 + threadIdx.x) / 8;                   \
+        const uint64_t nteams = uint64_t(gridDim.x) * 1024 / 8;                                  \
+        uint32_t acc = 0;                                                                        \
+        for (uint64_t rec = team; rec < count; rec += nteams)                                    \
+        {                                                                                        \
+            const uint8_t* r = base + rec * 4096 + tl * 16;                                      \
+            for (int g = 0; g < 4; g += 2)                                                       \
+            {                                                                                    \
+                u32x4 v[16];                                                                     \
+                _Pragma("unroll") for (int k = 0; k < 16; ++k)                                   \
+                    asm volatile("global_load_dwordx4 %0, %1, off " FLAGS                        \
+                                 : "=v"(v[k]) : "v"(r + g * 1024 + k * 128) : "memory");          \
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                 \
+                _Pragma("unroll") for (int k = 0; k < 16; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w; \
+            }                                                                                    \
+        }                                                                                        \
+        if (acc == 0x12345678u) sink[threadIdx.x] = acc;                                         \
+    }
+MI_PROBE_POLICY(probe_pol_none, "")
+MI_PROBE_POLICY(probe_pol_nt, "nt")
+MI_PROBE_POLICY(probe_pol_sc1, "sc1")
+MI_PROBE_POLICY(probe_pol_sc0sc1, "sc0 sc1")
+MI_PROBE_POLICY(probe_pol_ntsc1, "sc1 nt")
+MI_PROBE_POLICY(probe_pol_ntsc0sc1, "sc0 sc1 nt")
+MI_PROBE_POLICY(probe_pol_sc0nt, "sc0 nt")
+MI_PROBE_POLICY(probe_pol_sc0, "sc0")
+
+// The fixed kernel's pipeline with no compute: D groups of 8 rows in flight
+// per team, each consumed (XOR) when it lands (vmcnt(8 (D - 1))) and its
+// buffer refilled with the group D ahead (records strided by the team count,
+// 4 groups per 4 KiB record).  Explicit asm loads + waits, the waits tied to
+// the consumed registers so nothing is hoisted above them.
+template <int D>
+__global__ __launch_bounds__(1024, 1) void probe_pipe(const uint8_t* __restrict__ base,
+                                                      uint64_t count, uint32_t* __restrict__ sink)
+{
+    const uint32_t tl = threadIdx.x & 7;
+    const uint64_t team = (uint64_t(blockIdx.x) * 1024 + threadIdx.x) / 8;
+    const uint64_t nteams = uint64_t(gridDim.x) * 1024 / 8;
+    const uint64_t recs = (count - (team & ~uint64_t(7)) + nteams - 1) / nteams;  // per team
+    const uint64_t ngroups = recs * 4;
+    auto gaddr = [&](uint64_t q) {
+        uint64_t rec = team + (q >> 2) * nteams;
+        if (rec >= count) rec = count - 1;
+        return base + rec * 4096 + (q & 3) * 1024 + tl * 16;
+    };
+    u32x4 buf[D][8];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+    {
+        const uint8_t* p = gaddr(d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(buf[d][k]) : "v"(p + k * 128) : "memory");
+    }
+    for (uint64_t q = 0; q < ngroups; q += D)
+    {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+        {
+            asm volatile("s_waitcnt vmcnt(%8)"
+                         : "+v"(buf[d][0]), "+v"(buf[d][1]), "+v"(buf[d][2]), "+v"(buf[d][3]),
+                           "+v"(buf[d][4]), "+v"(buf[d][5]), "+v"(buf[d][6]), "+v"(buf[d][7])
+                         : "n"(8 * (D - 1)) : "memory");
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc ^= buf[d][k].x ^ buf[d][k].y ^ buf[d][k].z ^ buf[d][k].w;
+            const uint8_t* p = gaddr(q + d + D);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(buf[d][k]) : "v"(p + k * 128) : "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid, int reps,
@@ -120,6 +206,12 @@ extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid,
             case 9: hipLaunchKernelGGL((probe_teamN<8>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
             case 10: hipLaunchKernelGGL((probe_teamN<16>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
             case 11: hipLaunchKernelGGL((probe_teamN<2>), dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+#define MI_CASE(N, K) case N: hipLaunchKernelGGL(K, dim3(grid), dim3(1024), 0, 0, static_cast<const uint8_t*>(buf), bytes / 4096, sink); break;
+            MI_CASE(20, probe_pol_none) MI_CASE(21, probe_pol_nt) MI_CASE(22, probe_pol_sc1)
+            MI_CASE(23, probe_pol_sc0sc1) MI_CASE(24, probe_pol_ntsc1) MI_CASE(25, probe_pol_ntsc0sc1)
+            MI_CASE(26, probe_pol_sc0nt) MI_CASE(27, probe_pol_sc0)
+            MI_CASE(30, probe_pipe<1>) MI_CASE(31, probe_pipe<2>) MI_CASE(32, probe_pipe<3>)
+#undef MI_CASE
         }
     };
     launch();
