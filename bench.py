@@ -109,7 +109,7 @@ def pmc_traffic(args) -> tuple[float | None, str]:
                        stderr=subprocess.DEVNULL, cwd=out)
     except Exception as e:  # noqa: BLE001 -- traffic is optional, the bench is not
         return None, f"rocprofv3 pass failed: {e}"
-    fixed = args.config == "fixed4k"
+    fixed = args.config in ("fixed4k", "single")  # single: the fixed kernel on its 4 KiB chunks
     step_kernels = ("plan_", "long_items", "crc32c_chunk_kernel", "crc32c_finalize", "long_finalize")
     vals = []
     for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
@@ -271,6 +271,10 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
         gs = gold.get("single_record_seed0xc0de", {}).get("crc", {})
         data = E.DeviceBuffer(n + 4097)
         data.fill_splitmix64(SEED)
+        if args.child_pmc:
+            for _ in range(PMC_CHILD_STEPS):
+                E.crc32c_device(data, n)
+            return {}
         for _ in range(args.warmup):
             E.crc32c_device(data, n)
         t0 = time.perf_counter()
@@ -288,7 +292,9 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
                                    "head/tail windows and a two-level combine tree on the GPU"},
             "roofline": {"bound": "hbm", "achieved": round(n / wall / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(n / wall / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(n / wall / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic[0] is None else round(traffic[0]),
+                         "traffic_note": traffic[1] + " (crc32c_fixed_pipe_kernel, per call)",
                          "kernel": "crc32c_fixed_pipe_kernel + single_tree + single_join "
                                    "(whole call, host sync included)"},
             "digest_verified": ok, "crc": f"{got:#010x}"})
@@ -385,7 +391,7 @@ def main():
     # Traffic pass first, before this process touches the GPU.
     traffic, traffic_note = (None, "skipped")
     if rank == 0 and world == 1 and not args.child_pmc and not args.no_pmc and \
-            args.config in ("fixed4k", "zipf"):
+            args.config in ("fixed4k", "zipf", "single"):
         traffic, traffic_note = pmc_traffic(args)
 
     # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.

@@ -277,3 +277,33 @@ def test_device_single_buffer_sweep(engine, oracle):
             got = engine.crc32c_device(data, n, init_crc=init, offset=off)
             assert got == oracle.crc32c(init, host, n, off), (off, n, init)
     data.free()
+
+
+@pytest.mark.parametrize("shape", ["only_4_group", "only_short", "mixed_tiny"])
+def test_var_chunk_roles(engine, oracle, shape):
+    """The chunk launch gives all 16 waves to one role when the other has no
+    pieces: batches of 4 KiB-aligned 4 KiB records (only 4-group pieces),
+    of records under 1 KiB (only 1- and 2-group pieces), and a tiny mixed
+    batch whose grid is smaller than the chip."""
+    rng = np.random.default_rng(31)
+    if shape == "only_4_group":
+        count = 3000
+        lengths = np.full(count, 4096, dtype=np.uint32)
+        offsets = (np.arange(count, dtype=np.uint64) * 4096 + 8192).astype(np.uint64)
+    elif shape == "only_short":
+        count = 50000
+        lengths = rng.integers(32, 1000, count).astype(np.uint32)
+        # every record inside one 4 KiB chunk (a single piece of <= 9 rows)
+        offsets = (np.arange(count, dtype=np.uint64) * 4096 +
+                   rng.integers(0, 4096 - 1000, count).astype(np.uint64))
+    else:
+        count = 37
+        lengths = rng.integers(0, 20000, count).astype(np.uint32)
+        offsets = np.zeros(count, dtype=np.uint64)
+        offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    buf = rng.integers(0, 256, int((offsets + lengths).max()) + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32)
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
