@@ -24,7 +24,8 @@
 
 // Ablation modes for tools/ablate.py (the product build is mode 0):
 //   1 = skip the LDS table staging, 2 = no global loads (synthetic data),
-//   4 = no table lookups (data XORed straight into the chains).
+//   4 = no table lookups (data XORed straight into the chains),
+//   8 = address builds kept, each lookup replaced by one VALU op.
 // Results are wrong in any mode != 0; only the timing is meaningful.
 #ifndef MI_CRC_ABLATE
 #define MI_CRC_ABLATE 0
@@ -128,7 +129,8 @@ __device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint
         a[4 * q + 3] = __builtin_amdgcn_perm(li, V[q], 0x0C070305u);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) r[i] = lds32(kLdsMain + a[i]);
+    for (int i = 0; i < 16; ++i)
+        r[i] = (MI_CRC_ABLATE & 8) ? (a[i] ^ (a[i] >> 3)) : lds32(kLdsMain + a[i]);
     V[0] = xor3(xor3(r[0], r[1], r[2]), r[3], d.x);
     V[1] = xor3(xor3(r[4], r[5], r[6]), r[7], d.y);
     V[2] = xor3(xor3(r[8], r[9], r[10]), r[11], d.z);
