@@ -307,3 +307,42 @@ def test_var_chunk_roles(engine, oracle, shape):
                           oracle.batch(buf, offsets, lengths))
     assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits),
                           oracle.batch(buf, offsets, lengths, inits))
+
+
+def test_concurrent_callers(engine, oracle):
+    """consus::crc32c is called concurrently by the network threads
+    (txman/durable_log.cc:215-218, txman/main.cc:191-193): 12 threads, each
+    with its own engine stream and staging, mixing single buffers, batches
+    and fixed batches, every result checked."""
+    import threading
+    rng = np.random.default_rng(41)
+    buf = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    errors = []
+
+    def worker(t):
+        r = np.random.default_rng(100 + t)
+        try:
+            for _ in range(15):
+                off = int(r.integers(0, 1 << 20))
+                n = int(r.integers(0, 2 << 20))
+                init = int(r.integers(0, 2**32))
+                got = engine.crc32c(init, buf[off:off + n])
+                if got != oracle.crc32c(init, buf, n, off):
+                    errors.append(("buffer", t, off, n, init))
+                lens = r.integers(0, 9000, 200).astype(np.uint32)
+                offs = r.integers(0, (3 << 20) - 9000, 200).astype(np.uint64)
+                if not np.array_equal(engine.crc32c_batch(buf, offs, lens),
+                                      oracle.batch(buf, offs, lens, threads=1)):
+                    errors.append(("batch", t))
+                if not np.array_equal(engine.crc32c_fixed(buf, 4096, 4096, 256),
+                                      oracle.fixed(buf, 4096, 4096, 256)):
+                    errors.append(("fixed", t))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(("exception", t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
