@@ -59,11 +59,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="fixed4k",
-                    choices=["fixed4k", "zipf", "stream", "pcie4k", "single"],
+                    choices=["fixed4k", "zipf", "stream", "pcie4k", "single", "dlog"],
                     help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2]; "
                          "stream = configs[4] (64 MiB host segments, H2D+CRC+D2H); pcie4k = "
                          "configs[1] bytes starting in pinned host memory; single = the same "
-                         "4 GiB as ONE device-resident record (long-record path, SURVEY 8(f)4)")
+                         "4 GiB as ONE device-resident record (long-record path, SURVEY 8(f)4); "
+                         "dlog = the durable-log front-end (SURVEY 8(f)1): appends/s of 8 "
+                         "threads, GPU batch CRC per flushed segment")
     ap.add_argument("--segments", type=int, default=16, help="stream/pcie4k: segments per step")
     ap.add_argument("--records-per-rank", type=int, default=None,
                     help="default: 1M (configs[1]) on one GPU, 2M per GPU when N > 1, so that "
@@ -218,6 +220,41 @@ def cpu_baseline(args) -> dict:
                       f"{p1} passes single-thread + {pm} passes x {threads} std::threads, "
                       f"cpu: {model}",
             "first_crc": int(crc_ref[0])}
+
+
+def run_dlog(args) -> dict:
+    """The batching durable log driven as txman drives it (tools/dlog_bench.cc):
+    8 threads append 400K entries each (42-1024 B), the caller waits for the
+    watermark to cover them, then the log is replayed (GPU-verified scan of
+    both segment files) and every record checked byte-exact.  Segment files
+    on tmpfs (/dev/shm): fsync is free there, so this is the front-end and
+    GPU-batch rate, not a disk's."""
+    exe = os.path.join(REPO, "tools", "dlog_bench")
+    d = tempfile.mkdtemp(prefix="dlog_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    threads, per = 8, 400_000
+    runs = []
+    try:
+        for _ in range(max(1, args.steps // 10)):
+            r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(per), "42", "1024"],
+                               capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError(f"dlog_bench failed: {r.stdout[-500:]} {r.stderr[-500:]}")
+            runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+            shutil.rmtree(os.path.join(d, "log"), ignore_errors=True)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    best = max(runs, key=lambda x: x["appends_per_s"])
+    return {"metric": "durable-log appends/s, 8 appending threads, GPU batch CRC per flushed "
+                      "segment (txman/durable_log.cc append contract)",
+            "value": round(best["appends_per_s"], 1), "unit": "appends/s", "n_gpus": 1,
+            "steps": len(runs), "warmup": 0, "ms_per_step": round(best["durable_s"] * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: entry lengths uniform 42-1024 B, splitmix64 bytes",
+            "config": {"workload": f"{threads} threads x {per} appends, then wait for the "
+                                   f"watermark; segment files on tmpfs", "runs": runs},
+            "roofline": None, "cpu_baseline": None,
+            "digest_verified": all(x["replayed"] == x["appends"] and x["replay_bad"] == 0
+                                   for x in runs)}
 
 
 def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
@@ -394,10 +431,14 @@ def main():
             args.config in ("fixed4k", "zipf", "single"):
         traffic, traffic_note = pmc_traffic(args)
 
+    if args.config == "dlog":  # a child process drives the engine; none here
+        if rank == 0:
+            print(json.dumps(run_dlog(args)), flush=True)
+        return
+
     # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.
     import consus_amd as E
     E.init(0 if args.share_device else local)
-
     if args.config != "fixed4k":
         if world != 1:
             sys.exit("secondary configs run on one GPU")

@@ -30,6 +30,11 @@ int mi_dlog_error(mi_dlog* log);
 int64_t mi_dlog_replay(mi_dlog* log, void (*f)(void*, const unsigned char*, size_t), void* p);
 uint64_t mi_dlog_flushes(mi_dlog* log);
 uint64_t mi_dlog_frames_flushed(mi_dlog* log);
+/* Seconds the flush thread has spent, summed over flushes, in: [0] waiting
+ * for in-flight appends of a sealed segment, [1] walking the frame chain,
+ * [2] the batch CRC (GPU), [3] writing the CRCs into the frames, [4] pwrite,
+ * [5] fsync.  For tuning; any of out[0..5] may be read at any time. */
+void mi_dlog_flush_seconds(mi_dlog* log, double out[6]);
 
 /* Test hook (call before open): batch CRC engine other than the GPU. */
 typedef int (*mi_dlog_batch_crc)(void* ctx, const void* base, const uint64_t* offsets,

@@ -11,10 +11,12 @@
 //     (txman/durable_log.cc:54-61, 215-224), in two alternating segment files
 //     file_a / file_b created (truncated) by open() (:157-169);
 //   * durable() / wait() report the watermark "every recno < x is durable"
-//     (:421-440); the flush thread fsyncs the segment with the most unflushed
-//     bytes while appends go to the other one (:287-419).
-// What changes: append() copies the frame into the segment's staging buffer
-// (pinned host memory) and defers its CRC; the flush thread computes the CRCs
+//     (:421-440); one segment is fsynced while appends go to the other one
+//     (:287-419).
+// What changes: append() reserves its record number and staging offset with
+// one compare-and-swap on the active segment (no lock on the append path),
+// copies the frame into the segment's staging buffer (pinned host memory)
+// and defers its CRC; the flush thread computes the CRCs
 // of every staged frame of the segment in ONE GPU batch
 // (mi_crc32c_batch), patches them in, writes the segment with one pwrite and
 // fsyncs it before publishing the watermark -- so the watermark still covers
@@ -66,35 +68,42 @@ class durable_log
         // Counters for tests and tuning.
         uint64_t flushes() const;
         uint64_t frames_flushed() const;
+        // Seconds spent by the flush thread per phase: copy wait, frame
+        // walk, batch CRC, CRC patch, pwrite, fsync.
+        void flush_seconds(double out[6]) const;
 
     private:
         struct segment;
         void flush();
-        segment* select_segment_write();
-        segment* select_segment_fsync();
-        int64_t durable_lock_held_elsewhere();
-        int flush_segment(segment* seg, const std::vector<uint64_t>& offs,
-                          const std::vector<uint32_t>& lens, uint64_t used, uint64_t file_off);
+        int64_t append_slow(segment* seg);
+        void switch_to_next(segment* seg, uint64_t n);
+        int flush_segment(segment* seg, uint64_t nframes, uint64_t used);
 
     private:
         std::string m_path;
         int m_dir;
         int m_lock_fd;
-        std::mutex m_mtx;
+        std::mutex m_mtx;               // flush hand-offs, waiters; never on the append fast path
         std::condition_variable m_cond;
         std::thread m_flush;
-        int m_error;
+        std::atomic<int> m_error;
         bool m_wakeup;
         bool m_opened;
-        uint64_t m_next_entry;
         size_t m_capacity;
         segment* m_segment_a;
         segment* m_segment_b;
+        std::atomic<segment*> m_active;      // the segment appends reserve in
+        std::atomic<uint64_t> m_durable;     // every recno below it is on disk
+        std::atomic<bool> m_flush_idle;      // the flush thread sleeps for a first frame
         durable_log_batch_crc m_crc;
         void* m_crc_ctx;
         bool m_pinned;
         std::atomic<uint64_t> m_flushes;
         std::atomic<uint64_t> m_frames_flushed;
+        std::atomic<uint64_t> m_flush_ns[6];
+        std::vector<uint64_t> m_offs;   // flush thread: the sealed segment's frames
+        std::vector<uint32_t> m_lens;
+        std::vector<uint32_t> m_crcs;
 
     private:
         durable_log(const durable_log&);

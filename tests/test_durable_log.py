@@ -190,3 +190,35 @@ def test_scan_file_gpu(tmp_path):
         total += n
     assert total == 1000
     log.destroy()
+
+
+@pytest.mark.parametrize("capacity", [2048, 1 << 14])
+def test_concurrent_appenders_full_segments(make_log, tmp_path, capacity):
+    """Appends reserve with one atomic add on the active segment; when a frame
+    does not fit, it and every later reservation fail over to the next
+    segment.  Tiny staging buffers make that happen on most flushes: every
+    record must still be numbered densely, flushed, and replayed intact."""
+    log = make_log(capacity=capacity)
+    assert log.open(str(tmp_path / "d"))
+    got = {}
+    lock = threading.Lock()
+
+    def worker(t):
+        rng = np.random.default_rng(200 + t)
+        for i in range(400):
+            e = bytes([t, i & 255]) + rng.integers(0, 256, int(rng.integers(0, 700)),
+                                                   dtype=np.uint8).tobytes()
+            r = log.append(e)
+            assert r > 0
+            with lock:
+                got[r] = e
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert sorted(got) == list(range(1, 3201))
+    wait_durable(log, 3200)
+    assert log.frames_flushed() == 3200
+    log.close()
+    assert log.replay() == [got[i] for i in range(1, 3201)]

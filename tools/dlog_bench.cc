@@ -1,0 +1,172 @@
+// tools/dlog_bench.cc -- throughput of the batching durable-log front-end
+// (include/txman/durable_log.h; reference txman/durable_log.cc:187-242 append,
+// :287-347 flush) driven the way txman drives it: T network threads call
+// append() concurrently (txman/main.cc:191-193), then the caller waits for the
+// watermark to cover every record (daemon::durable, durable_log::wait).
+//
+//   dlog_bench DIR THREADS APPENDS_PER_THREAD MIN_ENTRY MAX_ENTRY [SEGMENT_BYTES]
+//
+// Entry lengths are uniform in [MIN_ENTRY, MAX_ENTRY] from a splitmix64
+// stream, entry bytes are slices of one splitmix64 pool.  After the timed
+// region the log is closed and replayed (a GPU-verified scan of both segment
+// files): every record must come back, in recno order, byte-exact.
+// Prints one JSON line.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "txman/durable_log.h"
+
+namespace {
+
+uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+double now()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Replay
+{
+    const std::vector<uint32_t>* len;  // entry length of recno r (1-based) at r - 1
+    const std::vector<uint64_t>* at;   // pool offset of recno r's entry
+    const unsigned char* pool;
+    uint64_t next = 0;
+    uint64_t bad = 0;
+};
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    if (argc < 6)
+    {
+        fprintf(stderr, "usage: %s DIR THREADS APPENDS_PER_THREAD MIN_ENTRY MAX_ENTRY [SEGMENT_BYTES]\n",
+                argv[0]);
+        return 2;
+    }
+    const std::string dir = argv[1];
+    const int threads = atoi(argv[2]);
+    const uint64_t per = strtoull(argv[3], nullptr, 10);
+    const uint32_t lo = uint32_t(atoi(argv[4])), hi = uint32_t(atoi(argv[5]));
+    const size_t seg = argc > 6 ? size_t(strtoull(argv[6], nullptr, 10)) : 0;
+    // diagnosis only: FAKE_CRC=1 replaces the GPU batch with a no-op (CRCs
+    // left zero, replay not checked) to time the front-end alone
+    const bool fake = getenv("FAKE_CRC") && atoi(getenv("FAKE_CRC"));
+    if (threads < 1 || per < 1 || hi < lo)
+    {
+        fprintf(stderr, "bad arguments\n");
+        return 2;
+    }
+    // entry pool: 64 MiB of splitmix64 bytes; entry k of thread t starts at a
+    // stream-chosen offset
+    const size_t pool_bytes = (64u << 20) + hi;
+    std::vector<unsigned char> pool(pool_bytes);
+    for (size_t i = 0; i < pool_bytes / 8; ++i)
+    {
+        const uint64_t w = splitmix64(0xD106ull ^ i);
+        memcpy(&pool[i * 8], &w, 8);
+    }
+    std::vector<std::vector<uint32_t>> lens(threads, std::vector<uint32_t>(per));
+    std::vector<std::vector<uint64_t>> offs(threads, std::vector<uint64_t>(per));
+    uint64_t entry_bytes = 0;
+    for (int t = 0; t < threads; ++t)
+        for (uint64_t k = 0; k < per; ++k)
+        {
+            const uint64_t r = splitmix64((uint64_t(t) << 40) ^ k ^ 0x5EEDull);
+            lens[t][k] = lo + uint32_t(r % (hi - lo + 1));
+            offs[t][k] = (r >> 20) % (pool_bytes - hi);
+            entry_bytes += lens[t][k];
+        }
+
+    consus::durable_log log(seg);
+    if (fake)
+        log.set_batch_crc_for_testing(
+            [](void*, const void*, const uint64_t*, const uint32_t*, size_t n, uint64_t,
+               uint32_t* out) {
+                memset(out, 0, n * 4);
+                return 0;
+            },
+            nullptr);
+    if (!log.open(dir))
+    {
+        fprintf(stderr, "open(%s) failed: %s\n", dir.c_str(), strerror(log.error()));
+        return 1;
+    }
+    // recno -> (thread, k) so the replay can be checked
+    const uint64_t total = uint64_t(threads) * per;
+    std::vector<uint32_t> rec_len(total);
+    std::vector<uint64_t> rec_at(total);
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false};
+    std::atomic<uint64_t> failures{0};
+    std::vector<std::thread> ths;
+    for (int t = 0; t < threads; ++t)
+        ths.emplace_back([&, t] {
+            ready.fetch_add(1);
+            while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+            for (uint64_t k = 0; k < per; ++k)
+            {
+                const int64_t r = log.append(&pool[offs[t][k]], lens[t][k]);
+                if (r <= 0 || uint64_t(r) > total)
+                {
+                    failures.fetch_add(1);
+                    continue;
+                }
+                rec_len[r - 1] = lens[t][k];
+                rec_at[r - 1] = offs[t][k];
+            }
+        });
+    while (ready.load() < threads) std::this_thread::yield();
+    const double t0 = now();
+    go.store(true, std::memory_order_release);
+    for (auto& th : ths) th.join();
+    const double t_appended = now();
+    int64_t x = log.durable();
+    while (x <= int64_t(total) && !log.error()) x = log.wait(x);
+    const double t_durable = now();
+    const uint64_t flushes = log.flushes(), frames = log.frames_flushed();
+    const int err = log.error();
+    double fs[6];
+    log.flush_seconds(fs);
+
+    // the replay: every record back, in order, byte-exact
+    Replay rp{&rec_len, &rec_at, pool.data()};
+    const int64_t n = fake ? int64_t(total) : log.replay(
+        [](void* p, const unsigned char* data, size_t len) {
+            Replay* r = static_cast<Replay*>(p);
+            const uint64_t i = r->next++;
+            if (i >= r->len->size() || len != (*r->len)[i] ||
+                memcmp(data, r->pool + (*r->at)[i], len) != 0)
+                ++r->bad;
+        },
+        &rp);
+    log.close();
+    const uint64_t frame_bytes = entry_bytes + total * 20;
+    printf("{\"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
+           "\"append_s\": %.6f, \"durable_s\": %.6f, \"appends_per_s\": %.1f, "
+           "\"frame_GiB_per_s\": %.4f, \"flushes\": %llu, \"frames_flushed\": %llu, "
+           "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
+           "\"flush_s\": {\"copy_wait\": %.4f, \"walk\": %.4f, \"batch_crc\": %.4f, "
+           "\"patch\": %.4f, \"pwrite\": %.4f, \"fsync\": %.4f}}\n",
+           threads, (unsigned long long)total, (unsigned long long)entry_bytes,
+           (unsigned long long)frame_bytes, t_appended - t0, t_durable - t0,
+           double(total) / (t_durable - t0), double(frame_bytes) / (t_durable - t0) / (1u << 30),
+           (unsigned long long)flushes, (unsigned long long)frames,
+           (unsigned long long)failures.load(), err, (long long)n, (unsigned long long)rp.bad,
+           fs[0], fs[1], fs[2], fs[3], fs[4], fs[5]);
+    return (failures.load() || err || n != int64_t(total) || rp.bad) ? 1 : 0;
+}
