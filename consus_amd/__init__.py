@@ -31,6 +31,7 @@ EHIP = -5
 ERCCL = -71
 FLAG_DEVICE = 0x1
 FLAG_ASYNC = 0x2
+FLAG_PLANNED = 0x4  # force plan -> chunks -> finalize (no one-launch direct kernel)
 MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D = 1, 2, 3
 
 
@@ -155,7 +156,7 @@ def zipf_lengths(seed: int, count: int, first: int = 0) -> np.ndarray:
     return out
 
 
-def crc32c_batch(buf, offsets, lengths, inits=None) -> np.ndarray:
+def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False) -> np.ndarray:
     """Per-record CRCs of host records [buf + off, +len)."""
     a = _as_u8(buf)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -168,7 +169,7 @@ def crc32c_batch(buf, offsets, lengths, inits=None) -> np.ndarray:
     out = np.zeros(off.size, dtype=np.uint32)
     _check(lib().mi_crc32c_batch(C.c_void_p(a.ctypes.data), _np_ptr(off), _np_ptr(ln),
                                  _np_ptr(ini), off.size, int(ln.sum(dtype=np.uint64)),
-                                 _np_ptr(out), 0), "mi_crc32c_batch")
+                                 _np_ptr(out), FLAG_PLANNED if planned else 0), "mi_crc32c_batch")
     return out
 
 

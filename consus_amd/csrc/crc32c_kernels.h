@@ -35,7 +35,8 @@ constexpr int kTabZInv128 = kTabP2 + 13 * 1024; // Z_{-128} = (Z_128)^{-1}
 constexpr int kTabZero = kTabZInv128 + 1024;    // 4 zero words (init 0 when inits == nullptr)
 constexpr int kTabFInit = kTabZero + 4;         // Z_n(0xFFFFFFFF), n = 0..4096 (init 0 seeds)
 constexpr int kTabZRows = kTabFInit + 4100;     // G^{128 k}, k = 1..32 (last-piece shifts)
-constexpr int kTabWords = kTabZRows + 32 * 1024;
+constexpr int kTabZNeg = kTabZRows + 32 * 1024; // Z_{-m} = (Z_m)^{-1}, m = 0..127 (direct kernel)
+constexpr int kTabWords = kTabZNeg + 128 * 1024;
 
 // LDS image of the record kernels (bytes).
 constexpr uint32_t kLdsMain = 0;            // 128 KiB bank-private G^{128}
@@ -76,6 +77,16 @@ struct VarWorkspace
     uint32_t* longs;      // count (records on the long path)
     uint64_t item_cap;
 };
+
+// Small batches: one launch, one team per record, no plan (launch_direct).
+constexpr uint64_t kDirectMaxCount = 1u << 18;   // records
+constexpr uint64_t kDirectMaxBytes = 32ull << 20;  // sum of lengths
+constexpr uint64_t kDirectMaxRecord = 16u << 10;   // longest record (128 rows for one team;
+                                                   // the planned path wins above ~32 KiB)
+hipError_t launch_direct(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint32_t* inits, uint64_t count, uint32_t* out,
+                         const uint32_t* tables, const uint32_t* pow2, int grid,
+                         hipStream_t stream);
 
 hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                            uint64_t count, const VarWorkspace& ws, hipStream_t stream);

@@ -1173,6 +1173,116 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Small batches (a durable-log flush, one consus::crc32c call on host data):
+// one launch instead of plan + chunks + finalize.  Team t of the grid takes
+// records t, t + nteams, ...; a record [a, E) is read as the 128-B rows that
+// cover it, bytes outside it masked to zero (leading zeros are free; the
+// m = ceil128(E) - E trailing ones are undone with one Z_{-m} table), folded
+// by the row update and team fold of the fixed kernel, and finished with the
+// seed: crc = ~(Z_L(~init) ^ raw).  Rows go 8 at a time (one load group).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
+    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
+    const uint32_t* __restrict__ pow2)
+{
+    stage_tables(tables);
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t li = lane_info();
+    const uint64_t team = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kTeam;
+    const uint64_t nteams = uint64_t(gridDim.x) * kBlock / kTeam;
+    const uint64_t team0 = team & ~uint64_t(7);  // first team of this wave
+    const uint64_t iters = team0 < count ? (count - team0 + nteams - 1) / nteams : 0;
+    const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
+    for (uint64_t it = 0; it < iters; ++it)
+    {
+        const uint64_t r_raw = team + it * nteams;
+        const bool live = r_raw < count;
+        const uint64_t r = live ? r_raw : count - 1;
+        const uint32_t L = live ? len[r] : 0u;
+        const uint64_t a = uint64_t(base) + off[r], E = a + L;
+        const uint64_t w0 = a & ~uint64_t(kRowBytes - 1);
+        const uint64_t w1 = (E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
+        const uint32_t rows = uint32_t((w1 - w0) / kRowBytes);
+        // groups of 8 rows, two buffers: group g + 1 is in flight while g is
+        // folded.  The wave runs as many groups as its longest record needs;
+        // rows past a record's end load a zero block and are not folded, so
+        // every load is unconditional and the vmcnt counts stay exact.
+        uint32_t ngw = (rows + kGroupRows - 1) / kGroupRows;
+        for (int dlt = 32; dlt >= 1; dlt >>= 1) ngw = max(ngw, uint32_t(__shfl_xor(int(ngw), dlt)));
+        auto load_group = [&](uint4 (&buf)[kGroupRows], uint32_t g) {
+#pragma unroll
+            for (int k = 0; k < kGroupRows; ++k)
+            {
+                const uint32_t row = g * kGroupRows + k;
+                const uint64_t bs = w0 + uint64_t(row) * kRowBytes + tl * 16;
+                buf[k] = load16(row < rows ? reinterpret_cast<const uint8_t*>(bs) : zero16);
+            }
+        };
+        uint32_t V[4] = {0, 0, 0, 0};
+        // only the first row starts before the record and only the last one
+        // runs past it: this lane keeps bytes >= f0 of the first, < bl of the last
+        const int32_t f0 = min(max(int32_t(a - w0) - int32_t(tl) * 16, 0), 16);
+        const int32_t bl = min(max(int32_t(E + kRowBytes - w1) - int32_t(tl) * 16, 0), 16);
+        auto fold_group = [&](const uint4 (&buf)[kGroupRows], uint32_t g) {
+#pragma unroll
+            for (int k = 0; k < kGroupRows; ++k)
+            {
+                const uint32_t row = g * kGroupRows + k;
+                if (row >= rows) break;
+                uint4 d = buf[k];
+                if (row == 0) d = mask_from(d, f0);
+                if (row + 1 == rows) d = mask_below(d, bl);
+                row_update(V, d, li);
+            }
+        };
+        uint4 A[kGroupRows], B[kGroupRows];
+        load_group(A, 0);
+        for (uint32_t g = 0; g < ngw; g += 2)
+        {
+            load_group(B, g + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            fold_group(A, g);
+            load_group(A, g + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            fold_group(B, g + 1);
+        }
+        const uint32_t W = team_fold(V);  // every lane of the wave takes part
+        if (tl == 0 && live)
+        {
+            const uint32_t raw = zglob(tables + kTabZNeg + uint32_t(w1 - E) * 1024, W);
+            const uint32_t init = inits ? inits[r] : 0u;
+            uint32_t seed;
+            if (init == 0 && L <= uint32_t(kChunk))
+                seed = tables[kTabFInit + L];  // Z_L(~0)
+            else
+            {
+                seed = ~init;
+                uint32_t n = L;
+                for (int k = 0; n; ++k, n >>= 1)
+                    if (n & 1u) seed = zglob(pow2 + k * 1024, seed);
+            }
+            out[r] = ~(seed ^ raw);
+        }
+    }
+}
+
+hipError_t launch_direct(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint32_t* inits, uint64_t count, uint32_t* out,
+                         const uint32_t* tables, const uint32_t* pow2, int grid,
+                         hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    const uint64_t need = (count + (kBlock / kTeam) - 1) / (kBlock / kTeam);
+    if (uint64_t(grid) > need) grid = int(need);
+    hipLaunchKernelGGL(crc32c_direct_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream,
+                       static_cast<const uint8_t*>(base), offsets, lengths, inits, count, out,
+                       tables, pow2);
+    return hipGetLastError();
+}
+
 // Offsets/lengths for a fixed-stride batch the fast kernel cannot take
 // (unaligned base/stride or a length that is not a multiple of 16).
 __global__ __launch_bounds__(256) void make_fixed_records_kernel(uint64_t* __restrict__ off,
@@ -1457,6 +1567,9 @@ hipError_t configure_kernels()
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_chunk_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_direct_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),

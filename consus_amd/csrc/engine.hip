@@ -113,6 +113,10 @@ int init_device(int device)
             return fail(MI_CRC32C_EHIP, "Z_128 is not invertible (table construction bug)");
         }
         make_op_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZInv128]), inv);
+        // Z_{-m} = Z_{-128} o Z_{128-m}, m = 0..127 (m = 0: the identity)
+        for (int m = 0; m < kRowBytes; ++m)
+            make_op_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZNeg + m * 1024]),
+                           m ? zeros_op(uint64_t(kRowBytes - m)).then(inv) : Op32::identity());
     }
     {
         // F[n] = Z_n(~0): the register a zero init reaches after n bytes of zeros
@@ -249,13 +253,23 @@ uint32_t apply_zeros(const DeviceState* d, uint32_t s, uint64_t n)
 // All pointers device pointers; enqueued on c->stream.  `total_bytes` bounds
 // the plan size (0 = unknown -> one read-back).
 int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
-            const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
+            const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
+            uint64_t max_len = UINT64_MAX)  // longest record if known (host batches)
 {
     if (count == 0) return MI_CRC32C_OK;
     if (count >= (1ull << 31)) return fail(MI_CRC32C_EINVAL, "count >= 2^31 records");
     // items pack addresses in 41 bits (crc32c_kernels.h: Item); user-space and
     // GPU virtual addresses are below 2^47
     if (uintptr_t(base) >= (kItemMaxAddr >> 1)) return fail(MI_CRC32C_EINVAL, "address above 2^47");
+    // small batches of short records: one launch, no plan (a durable-log
+    // flush, one host call); a team hashes a record's rows serially, so only
+    // when the longest record is known to be short
+    if (max_len <= kDirectMaxRecord && total_bytes <= kDirectMaxBytes && count <= kDirectMaxCount)
+    {
+        HIP_TRY(launch_direct(base, off, len, inits, count, out, d->d_tables, d->d_pow2, d->cus,
+                              c->stream));
+        return MI_CRC32C_OK;
+    }
     const uint32_t nb = var_plan_blocks(count);
     int st;
     if ((st = c->blk.reserve((kBins * size_t(nb) + kPlanHdrWords) * 4)) ||
@@ -384,13 +398,14 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
         return finish(c, flags);
     }
     // Host batch: stage the spanned bytes, rebased offsets, lengths, inits.
-    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
+    uint64_t lo = UINT64_MAX, hi = 0, total = 0, maxlen = 0;
     for (size_t i = 0; i < count; ++i)
     {
         if (lengths[i] == 0) continue;
         lo = std::min<uint64_t>(lo, offsets[i]);
         hi = std::max<uint64_t>(hi, offsets[i] + lengths[i]);
         total += lengths[i];
+        maxlen = std::max<uint64_t>(maxlen, lengths[i]);
     }
     if (lo == UINT64_MAX) lo = hi = 0;
     if (hi > lo && !base) return fail(MI_CRC32C_EINVAL, "null base");
@@ -409,7 +424,7 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
         HIP_TRY(hipMemcpyAsync(c->inits.p, inits, count * 4, hipMemcpyHostToDevice, c->stream));
     if ((st = run_var(d, c, c->data.p, c->off.as<uint64_t>(), c->len.as<uint32_t>(),
                       inits ? c->inits.as<uint32_t>() : nullptr, count, total,
-                      c->out.as<uint32_t>())))
+                      c->out.as<uint32_t>(), (flags & MI_CRC32C_PLANNED) ? UINT64_MAX : maxlen)))
         return st;
     HIP_TRY(hipMemcpyAsync(out, c->out.p, count * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));

@@ -40,6 +40,10 @@ extern "C" {
 #define MI_CRC32C_DEVICE 0x1u   /* pointer arguments are device pointers */
 #define MI_CRC32C_ASYNC 0x2u    /* DEVICE only: return once enqueued on the
                                    calling thread's stream (mi_crc32c_stream_sync) */
+#define MI_CRC32C_PLANNED 0x4u  /* mi_crc32c_batch on host memory: always take the
+                                   planned path (plan -> chunks -> finalize), even
+                                   for a batch of short records small enough for
+                                   the one-launch direct kernel (tests, tuning) */
 
 /* ---- engine ------------------------------------------------------------- */
 /* Select the device and upload the operator tables.  Idempotent; called

@@ -59,28 +59,35 @@ def test_fixed_shapes(engine, oracle, length, stride):
     assert np.array_equal(got, oracle.fixed(buf, stride, length, count, inits=inits))
 
 
-def test_var_random_lengths(engine, oracle):
+# Host batches of short records take the one-launch direct kernel; planned=True
+# forces plan -> chunks -> finalize on the same inputs.
+PATHS = pytest.mark.parametrize("planned", [False, True], ids=["direct", "planned"])
+
+
+@PATHS
+def test_var_random_lengths(engine, oracle, planned):
     rng = np.random.default_rng(3)
     count = 4000
-    lengths = rng.integers(0, 20000, count).astype(np.uint32)
+    lengths = rng.integers(0, 20000 if planned else 16385, count).astype(np.uint32)
     lengths[::7] = rng.integers(0, 40, lengths[::7].size)
     offsets = np.zeros(count, dtype=np.uint64)
     offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
     buf = rng.integers(0, 256, int(lengths.sum()) + 1, dtype=np.uint8)
     inits = rng.integers(0, 2**32, count, dtype=np.uint32)
-    got = engine.crc32c_batch(buf, offsets, lengths)
+    got = engine.crc32c_batch(buf, offsets, lengths, planned=planned)
     assert np.array_equal(got, oracle.batch(buf, offsets, lengths))
-    got = engine.crc32c_batch(buf, offsets, lengths, inits)
+    got = engine.crc32c_batch(buf, offsets, lengths, inits, planned=planned)
     assert np.array_equal(got, oracle.batch(buf, offsets, lengths, inits))
 
 
-def test_var_unordered_overlapping(engine, oracle):
+@PATHS
+def test_var_unordered_overlapping(engine, oracle, planned):
     rng = np.random.default_rng(4)
     buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
     count = 3000
-    lengths = rng.integers(0, 70000, count).astype(np.uint32)
+    lengths = rng.integers(0, 70000 if planned else 16385, count).astype(np.uint32)
     offsets = np.array([rng.integers(0, buf.size - L + 1) for L in lengths], dtype=np.uint64)
-    got = engine.crc32c_batch(buf, offsets, lengths)
+    got = engine.crc32c_batch(buf, offsets, lengths, planned=planned)
     assert np.array_equal(got, oracle.batch(buf, offsets, lengths))
 
 
@@ -210,7 +217,8 @@ def test_var_many_records_multi_tile_plan(engine, oracle):
     assert np.array_equal(got, oracle.batch(host, offsets, lengths))
 
 
-def test_var_alignment_sweep(engine, oracle):
+@PATHS
+def test_var_alignment_sweep(engine, oracle, planned):
     """Every start residue mod 128 and starts just before 4 KiB boundaries,
     with lengths at row (128 B), group (1 KiB) and chunk (4 KiB) edges, with
     and without inits: the masking, bin and window-shift cases of the plan."""
@@ -220,6 +228,8 @@ def test_var_alignment_sweep(engine, oracle):
     lens = [1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 127, 128, 129, 255, 256, 257, 511,
             512, 513, 1023, 1024, 1025, 2047, 2048, 2049, 3071, 3072, 3073, 4095, 4096, 4097,
             8191, 8192, 8193, 12289, 70000]
+    if not planned:  # the direct kernel takes batches whose records are all <= 16 KiB
+        lens = [n for n in lens if n <= 16384]
     offsets, lengths = [], []
     for i, s in enumerate(starts):
         for j, n in enumerate(lens):
@@ -229,9 +239,9 @@ def test_var_alignment_sweep(engine, oracle):
     lengths = np.array(lengths, dtype=np.uint32)
     buf = rng.integers(0, 256, int((offsets + lengths).max()) + 64, dtype=np.uint8)
     inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
-    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths),
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, planned=planned),
                           oracle.batch(buf, offsets, lengths))
-    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits),
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits, planned=planned),
                           oracle.batch(buf, offsets, lengths, inits))
 
 
@@ -303,9 +313,9 @@ def test_var_chunk_roles(engine, oracle, shape):
         offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
     buf = rng.integers(0, 256, int((offsets + lengths).max()) + 64, dtype=np.uint8)
     inits = rng.integers(0, 2**32, count, dtype=np.uint32)
-    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths),
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, planned=True),
                           oracle.batch(buf, offsets, lengths))
-    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits),
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, inits, planned=True),
                           oracle.batch(buf, offsets, lengths, inits))
 
 
