@@ -688,12 +688,13 @@ int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, s
     auto& s = p->slots[t % p->slots.size()];
     int st;
     if ((st = slot_complete(s))) return st;
-    uint64_t total = 0;
+    uint64_t total = 0, maxlen = 0;
     for (size_t i = 0; i < count; ++i)
     {
         if (lengths[i] && offsets[i] + lengths[i] > bytes)
             return fail(MI_CRC32C_EINVAL, "record outside segment");
         total += lengths[i];
+        maxlen = std::max<uint64_t>(maxlen, lengths[i]);
     }
     const void* src = host_segment;
     if (bytes && !is_pinned(host_segment))
@@ -713,7 +714,7 @@ int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, s
     if ((st = run_var(d, &c, s.dseg.p, reinterpret_cast<uint64_t*>(dm),
                       reinterpret_cast<uint32_t*>(dm + count * 8),
                       inits ? reinterpret_cast<uint32_t*>(dm + count * 12) : nullptr, count, total,
-                      c.out.as<uint32_t>())))
+                      c.out.as<uint32_t>(), maxlen)))
         return st;
     HIP_TRY(hipMemcpyAsync(s.res.p, c.out.p, count * 4, hipMemcpyDeviceToHost, c.stream));
     HIP_TRY(hipEventRecord(c.done, c.stream));

@@ -115,10 +115,12 @@ def make_frames(rng, nbytes, max_entry=20000):
         np.array(lens, np.uint32)
 
 
-def test_pipeline_segments_pageable_and_pinned(engine, oracle):
+@pytest.mark.parametrize("max_entry", [20000, 2000], ids=["planned", "direct"])
+def test_pipeline_segments_pageable_and_pinned(engine, oracle, max_entry):
+    """Segments whose entries are all <= 16 KiB take the direct kernel."""
     rng = np.random.default_rng(8)
-    segs = [make_frames(rng, 4 << 20) for _ in range(5)]
-    p = engine.Pipeline(4 << 20, 4096, depth=2)
+    segs = [make_frames(rng, 4 << 20, max_entry) for _ in range(5)]
+    p = engine.Pipeline(4 << 20, 16384, depth=2)
     outs, tickets = [], []
     pinned = engine.PinnedBuffer(4 << 20)
     for i, (buf, off, ln) in enumerate(segs):
