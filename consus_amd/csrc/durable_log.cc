@@ -6,7 +6,7 @@
 // flush thread with all signals blocked (:287-347) that fsyncs one segment
 // while appends go to the other, and the watermark "every recno < x is
 // durable" (:421-440).  Changed: append() reserves (record number, staging
-// offset) with one compare-and-swap on the active segment instead of two
+// offset) with one fetch-and-add on the active segment instead of two
 // m_mtx sections (:195-213, :232-239) -- under 8 appending threads the lock
 // hand-offs cut throughput ~9x -- and stages the frame in pinned memory; the
 // flush thread checksums each sealed segment in one GPU batch, then writes it
@@ -157,12 +157,12 @@ bool read_file(int dirfd, const char* name, std::vector<unsigned char>* out)
 }  // namespace
 
 // Reservation word of a segment: bit 63 = sealed (no more appends), bits
-// 40..62 = frames reserved, bits 0..39 = staged bytes reserved.  Appends take
-// their slot with one compare-and-swap; frames therefore sit back to back in
-// the arena in reservation order, and frame i has record number base + i.
-// Reservations are one fetch-and-add (under 8-16 appending threads a
-// compare-and-swap loop measured half the append rate); when the segment
-// fills, the adds past the end fail and the first failure marks the cut.
+// 40..62 = frames reserved, bits 0..39 = staged bytes reserved.  An append
+// takes its slot with one fetch-and-add (under 8-16 appending threads a
+// compare-and-swap loop measured half the append rate), so frames sit back
+// to back in the arena in reservation order and frame i has record number
+// base + i.  When the segment fills, the adds past the end fail and the
+// first failure marks the cut.
 constexpr uint64_t kSealed = uint64_t(1) << 63;
 constexpr int kIdxShift = 40;
 constexpr uint64_t kUsedMask = (uint64_t(1) << kIdxShift) - 1;
@@ -185,9 +185,9 @@ struct durable_log::segment
     uint64_t* at = nullptr;
     uint64_t slots = 0;              // capacity in frames (a multiple of 8)
     uint64_t& at_slot(uint64_t i) { return at[(i & 7) * (slots >> 3) + (i >> 3)]; }
-    std::atomic<uint64_t> word{kSealed};
+    alignas(64) std::atomic<uint64_t> word{kSealed};  // every append's one atomic: own line
     // (index << 40) | offset of the first reservation that did not fit
-    std::atomic<uint64_t> cut{~uint64_t(0)};
+    alignas(64) std::atomic<uint64_t> cut{~uint64_t(0)};
     std::atomic<uint64_t> failed{0};  // reservations that did not fit
     // frames whose bytes are fully staged, counted in per-thread shards on
     // lines of their own (a single counter was a second contended line per

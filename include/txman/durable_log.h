@@ -14,7 +14,7 @@
 //     (:421-440); one segment is fsynced while appends go to the other one
 //     (:287-419).
 // What changes: append() reserves its record number and staging offset with
-// one compare-and-swap on the active segment (no lock on the append path),
+// one fetch-and-add on the active segment (no lock on the append path),
 // copies the frame into the segment's staging buffer (pinned host memory)
 // and defers its CRC; the flush thread computes the CRCs
 // of every staged frame of the segment in ONE GPU batch
