@@ -1,0 +1,87 @@
+"""Seeded random batches against the oracle (bit-exact), through every
+variable-length entry point: host batches on the direct kernel and on the
+planned path, device batches with and without the size hint, fixed-stride
+batches, and single buffers (host and device).  Shapes mix empty, tiny,
+row- and chunk-edge, and multi-chunk records; offsets packed, random,
+overlapping and unordered; inits random or absent.
+
+FUZZ_ROUNDS (environment) raises the number of rounds for longer soaks.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROUNDS = int(os.environ.get("FUZZ_ROUNDS", "24"))
+
+
+def random_lengths(rng, count):
+    kind = rng.integers(0, 5)
+    if kind == 0:
+        return rng.integers(0, 40, count)
+    if kind == 1:
+        return rng.integers(0, 5000, count)
+    if kind == 2:  # around row / group / chunk edges
+        edges = np.array([127, 128, 129, 1023, 1024, 1025, 4095, 4096, 4097, 8192])
+        return edges[rng.integers(0, edges.size, count)] + rng.integers(-2, 3, count)
+    if kind == 3:
+        return rng.integers(0, 70000, count)
+    return np.minimum(rng.zipf(1.3, count) * 64, 300000)
+
+
+@pytest.mark.parametrize("round_", range(ROUNDS))
+def test_fuzz_round(engine, oracle, round_):
+    rng = np.random.default_rng(9000 + round_)
+    count = int(rng.integers(1, 3000))
+    lengths = np.clip(random_lengths(rng, count), 0, None).astype(np.uint32)
+    layout = rng.integers(0, 3)
+    if layout == 0:  # packed back to back from a random start
+        offsets = np.zeros(count, dtype=np.uint64)
+        offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+        offsets += np.uint64(rng.integers(0, 4096))
+        size = int(offsets[-1] + lengths[-1]) + 64
+    else:  # random, possibly overlapping, unordered
+        size = int(lengths.max()) + int(rng.integers(1, 1 << 20))
+        offsets = np.array([rng.integers(0, size - int(L) + 1) for L in lengths], dtype=np.uint64)
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32) if rng.integers(0, 2) else None
+    want = oracle.batch(buf, offsets, lengths, inits)
+
+    # host batches: direct kernel when every record is short, and the planned path
+    for planned in (False, True):
+        got = engine.crc32c_batch(buf, offsets, lengths, inits, planned=planned)
+        assert np.array_equal(got, want), ("host", planned)
+
+    # device batch, with the size hint and without it (plan read-back)
+    data = engine.DeviceBuffer(size)
+    data.upload(buf)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    d_ini = None
+    if inits is not None:
+        d_ini = engine.DeviceBuffer(count * 4)
+        d_ini.upload(inits)
+    for hint in (int(lengths.sum(dtype=np.uint64)), 0):
+        engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini, total_bytes=hint)
+        assert np.array_equal(d_out.download(np.uint32, count), want), ("device", hint)
+
+    # single buffers: one record on the host and on the device
+    i = int(rng.integers(0, count))
+    o, L = int(offsets[i]), int(lengths[i])
+    init = int(inits[i]) if inits is not None else 0
+    assert engine.crc32c(init, buf[o:o + L]) == int(want[i])
+    assert engine.crc32c_device(data, L, init_crc=init, offset=o) == int(want[i])
+
+    # a fixed-stride batch over the same bytes
+    stride = int(rng.integers(1, 5000))
+    flen = int(rng.integers(0, stride + 1))
+    fcount = max(1, min(500, (size - flen) // stride))
+    fini = rng.integers(0, 2**32, fcount, dtype=np.uint32) if rng.integers(0, 2) else None
+    assert np.array_equal(engine.crc32c_fixed(buf, stride, flen, fcount, inits=fini),
+                          oracle.fixed(buf, stride, flen, fcount, inits=fini)), (stride, flen)
+    for b in (data, d_off, d_len, d_out) + ((d_ini,) if d_ini is not None else ()):
+        b.free()
