@@ -11,9 +11,10 @@ txman/durable_log.cc:215-218) -- done by the HIP kernels through the C ABI
 Workload (N=1): BASELINE.json configs[1] -- 1M x 4 KiB records resident in
 HBM, bytes = splitmix64 stream of seed 0xC0DE, generated on
 the device before timing.  N>1 (torchrun, one process per GPU): every rank
-owns its own 1M-record shard of the same global stream (record offset
-rank*R), so per-GPU work is fixed ("scaling": "weak") and no collective runs
-inside the timed region (records are independent).  After
+owns its own 2M-record shard of the same global stream (record offset
+rank*R; N = 8 is configs[3], 16M x 4 KiB), so per-GPU work is fixed
+("scaling": "weak") and no collective runs inside the timed region (records
+are independent).  After
 timing, every rank's CRC vector is reduced on its GPU to a digest; the
 digests are compared with the committed golden values (tests/golden).
 
@@ -25,7 +26,8 @@ The JSON line also carries
                 reports half of wide streaming reads, MI355X_MICROARCH.md HBM)
   cpu_baseline  the reference common/crc32c.cc itself (oracle/_ref, compiled
                 unmodified) on the host cores, over a bounded sample of the
-                same records (rank 0, N=1 only)
+                same records (rank 0, N=1 only): its dispatched path single-
+                threaded and on up to 16 threads, and its slicing-by-8 path once
 """
 from __future__ import annotations
 
@@ -203,6 +205,11 @@ def cpu_baseline(args) -> dict:
     crc_ref = ref.fixed(buf, L, L, 64, threads=1)
     single, p1 = rate(1)
     multi, pm = rate(threads)
+    # the reference's other path, slicing-by-8 (common/crc32c.cc:40-48, 594-634;
+    # taken on CPUs without SSE4.2), once over 256 MiB of the sample
+    t0 = time.perf_counter()
+    ref.crc32c(0, buf, 256 << 20, impl="sw")
+    sb8 = (256 << 20) / (time.perf_counter() - t0) / 2**30
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -214,6 +221,7 @@ def cpu_baseline(args) -> dict:
         pass
     return {"value": round(multi, 2), "unit": "GiB/s", "cores": threads, "kind": "reference",
             "single_thread_value": round(single, 2),
+            "slicing_by_8_single_thread_value": round(sb8, 2),
             "sample": f"first {n} of the same {L}-B records ({n * L >> 20} MiB, host DRAM), "
                       f"consus::crc32c from common/crc32c.cc compiled unmodified "
                       f"(dispatch {'sse42 crc32q' if ref.lib.ref_dispatch_is_sse42() else 'slicing-by-8'}), "
