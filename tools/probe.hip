@@ -181,6 +181,57 @@ __global__ __launch_bounds__(1024, 1) void probe_pipe(const uint8_t* __restrict_
     if (acc == 0x12345678u) sink[threadIdx.x] = acc;
 }
 
+// probe_pipe<2> with an XCD-contiguous record map: workgroups are dealt to
+// the 8 XCDs round-robin (b % 8), so workgroup b is renumbered to
+// (b % 8) * (grid / 8) + b / 8 and each XCD sweeps one contiguous eighth of
+// the records instead of interleaved 128-record stretches.
+__global__ __launch_bounds__(1024, 1) void probe_pipe_xcd(const uint8_t* __restrict__ base,
+                                                          uint64_t count, uint32_t* __restrict__ sink)
+{
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t vb = (b % 8) * (G / 8) + b / 8;
+    const uint32_t tl = threadIdx.x & 7;
+    const uint64_t team = (uint64_t(vb) * 1024 + threadIdx.x) / 8;
+    const uint64_t nteams = uint64_t(G) * 1024 / 8;
+    // contiguous: team t owns records [t * per, (t + 1) * per)
+    const uint64_t per = count / nteams;
+    u32x4 buf[2][8];
+    uint32_t acc = 0;
+    auto gaddr = [&](uint64_t q) {
+        uint64_t rec = team * per + (q >> 2);
+        if (rec >= count) rec = count - 1;
+        return base + rec * 4096 + (q & 3) * 1024 + tl * 16;
+    };
+    const uint64_t ngroups = per * 4;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+    {
+        const uint8_t* p = gaddr(d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(buf[d][k]) : "v"(p + k * 128) : "memory");
+    }
+    for (uint64_t q = 0; q < ngroups; q += 2)
+    {
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+        {
+            asm volatile("s_waitcnt vmcnt(8)"
+                         : "+v"(buf[d][0]), "+v"(buf[d][1]), "+v"(buf[d][2]), "+v"(buf[d][3]),
+                           "+v"(buf[d][4]), "+v"(buf[d][5]), "+v"(buf[d][6]), "+v"(buf[d][7])
+                         :: "memory");
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc ^= buf[d][k].x ^ buf[d][k].y ^ buf[d][k].z ^ buf[d][k].w;
+            const uint8_t* p = gaddr(q + d + 2);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(buf[d][k]) : "v"(p + k * 128) : "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
 }  // namespace
 
 extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid, int reps,
@@ -211,6 +262,7 @@ extern "C" float probe_run(int which, const void* buf, uint64_t bytes, int grid,
             MI_CASE(23, probe_pol_sc0sc1) MI_CASE(24, probe_pol_ntsc1) MI_CASE(25, probe_pol_ntsc0sc1)
             MI_CASE(26, probe_pol_sc0nt) MI_CASE(27, probe_pol_sc0)
             MI_CASE(30, probe_pipe<1>) MI_CASE(31, probe_pipe<2>) MI_CASE(32, probe_pipe<3>)
+            MI_CASE(33, probe_pipe_xcd)
 #undef MI_CASE
         }
     };

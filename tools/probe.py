@@ -26,9 +26,11 @@ names = {0: "stream plain U8", 1: "stream nt U8", 2: "stream plain U16", 3: "tea
          8: "team4 nt", 9: "team8 nt", 10: "team16 nt", 11: "team2 nt",
          20: "asm none", 21: "asm nt", 22: "asm sc1", 23: "asm sc0 sc1", 24: "asm sc1 nt",
          25: "asm sc0 sc1 nt", 26: "asm sc0 nt", 27: "asm sc0",
-         30: "pipe D=1", 31: "pipe D=2", 32: "pipe D=3"}
+         30: "pipe D=1", 31: "pipe D=2", 32: "pipe D=3", 33: "pipe D=2 XCD-contig"}
 if "--pipe" in sys.argv:
     plan = [(w, (256,)) for w in (30, 31, 32, 4)] * 3
+elif "--xcd" in sys.argv:
+    plan = [(w, (256,)) for w in (31, 33)] * 4
 elif "--policy" in sys.argv:
     plan = [(w, (256,)) for w in (20, 21, 22, 23, 24, 25, 26, 27, 4)] * 2
 else:
