@@ -358,3 +358,49 @@ def test_concurrent_callers(engine, oracle):
     for th in ths:
         th.join()
     assert not errors, errors[:5]
+
+
+def _gold(name):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")) as f:
+        return json.load(f)[name]
+
+
+def test_full_config3_16M_records_one_gpu(engine):
+    """BASELINE configs[3]'s whole record set (16M x 4 KiB = 64 GiB) in one
+    launch on one GPU: record offsets past 2^32 and 2^36 bytes, 16 golden
+    block digests (crc32c of each 1M-record block's CRC vector)."""
+    g = _gold("fixed_4096_seed0xc0de_per_1048576")
+    n = 16 << 20
+    data = engine.DeviceBuffer(n * 4096)
+    out = engine.DeviceBuffer(n * 4)
+    data.fill_splitmix64(0xC0DE)
+    engine.device_batch_fixed(data, 4096, 4096, n, out)
+    per = (1 << 20) * 4
+    got = [engine.crc32c_device(out, per, offset=k * per) for k in range(16)]
+    assert got == g["block_digests"]
+    data.free()
+    out.free()
+
+
+def test_full_config2_zipf_golden(engine):
+    """BASELINE configs[2] at full size (1M Zipf records, 4.9 GB) through
+    the device batch, with and without the size hint, against the golden
+    digest of the reference's CRC vector."""
+    from consus_amd import workload as W
+    g = _gold("zipf_seed0x5eed_data0xda7a5eed_1048576")
+    R = 1 << 20
+    off, ln, total = W.zipf_records(R)
+    assert total == g["total_bytes"]
+    data = engine.DeviceBuffer(total + 16)
+    data.fill_splitmix64(W.DATA_SEED)
+    d_off, d_len, out = engine.DeviceBuffer(R * 8), engine.DeviceBuffer(R * 4), engine.DeviceBuffer(R * 4)
+    d_off.upload(off)
+    d_len.upload(ln)
+    for hint in (total, 0):
+        out.memset(0)
+        engine.device_batch(data, d_off, d_len, R, out, total_bytes=hint)
+        assert engine.crc32c_device(out, R * 4) == g["digest"], hint
+    for b in (data, d_off, d_len, out):
+        b.free()
