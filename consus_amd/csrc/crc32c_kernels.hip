@@ -25,7 +25,8 @@
 // Ablation modes for tools/ablate.py (the product build is mode 0):
 //   1 = skip the LDS table staging, 2 = no global loads (synthetic data),
 //   4 = no table lookups (data XORed straight into the chains),
-//   8 = address builds kept, each lookup replaced by one VALU op.
+//   8 = address builds kept, each lookup replaced by one VALU op,
+//   16 = team fold replaced by an XOR of the chains.
 // Results are wrong in any mode != 0; only the timing is meaningful.
 #ifndef MI_CRC_ABLATE
 #define MI_CRC_ABLATE 0
@@ -141,12 +142,23 @@ __device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint
 // last processed row ends exactly at the end of those bytes.  Valid in lane
 // (lane & 7) == 0 of the team.  DESIGN.md section 3.2:
 //   raw = XOR_L Z_{16(7-L)}( Z16 V0 ^ Z12 V1 ^ Z8 V2 ^ Z4 V3 )_L
+// v from lane + N of the same 16-lane DPP row (row_shl:N); a team's lane 0
+// (lane 0 or 8 of a row) reads lanes 1..7 of its own team.  A DPP operand
+// costs nothing beside its v_xor; __shfl_xor is a ds_bpermute round trip
+// (measured: 0.657 vs 0.657-0.665 ms on the headline batch).
+template <int N>
+__device__ __forceinline__ uint32_t from_lane_up(uint32_t v)
+{
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x100 + N, 0xF, 0xF, true));
+}
+
 __device__ __forceinline__ uint32_t team_fold(const uint32_t (&V)[4])
 {
+    if (MI_CRC_ABLATE & 16) return V[0] ^ V[1] ^ V[2] ^ V[3];
     const uint32_t x = zT<4>(V[0]) ^ zT<3>(V[1]) ^ zT<2>(V[2]) ^ zT<1>(V[3]);
-    const uint32_t y = zT<4>(x) ^ __shfl_xor(x, 1);
-    const uint32_t w = zG(kLdsZ32, y) ^ __shfl_xor(y, 2);
-    return zG(kLdsZ64, w) ^ __shfl_xor(w, 4);
+    const uint32_t y = zT<4>(x) ^ from_lane_up<1>(x);
+    const uint32_t w = zG(kLdsZ32, y) ^ from_lane_up<2>(y);
+    return zG(kLdsZ64, w) ^ from_lane_up<4>(w);
 }
 
 // Record bytes are read exactly once: non-temporal loads (global_load_dwordx4
