@@ -65,7 +65,8 @@ def parse():
                     help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2]; "
                          "stream = configs[4] (64 MiB host segments, H2D+CRC+D2H); pcie4k = "
                          "configs[1] bytes starting in pinned host memory; single = the same "
-                         "4 GiB as ONE device-resident record (long-record path, SURVEY 8(f)4); "
+                         "4 GiB as ONE device-resident record (long-record path, SURVEY 8(f)4; "
+                         "at N > 1 one N x 4 GiB record split across the GPUs, SURVEY 8(e)); "
                          "dlog = the durable-log front-end (SURVEY 8(f)1): appends/s of 8 "
                          "threads, GPU batch CRC per flushed segment")
     ap.add_argument("--segments", type=int, default=16, help="stream/pcie4k: segments per step")
@@ -422,6 +423,62 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
     return res
 
 
+def run_single_split(args, E, dist, rank, world):
+    """One record of world x 4 GiB, rank r holding bytes [4 GiB r, 4 GiB (r+1))
+    of stream 0xC0DE in its HBM (a record split across GPUs).
+    Timed: each rank's synchronous crc32c(0, slice), between barriers, max
+    over ranks.  After the timed region the (crc, length) pairs -- 8 bytes
+    per rank -- are gathered and folded with the combine operator on rank 0
+    (timed once, reported as "exchange_ms") and checked against the golden
+    CRC of the whole record."""
+    import torch
+    from consus_amd import shard
+    n = 1 << 32
+    start, length = shard.record_slices(world * n, world)[rank]
+    data = E.DeviceBuffer(length)
+    data.fill_splitmix64(SEED, byte_offset=start)
+    for _ in range(args.warmup):
+        E.crc32c_device(data, length)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        crc = E.crc32c_device(data, length)  # synchronous: kernels + 4-byte read-back
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t[0])
+    t1 = time.perf_counter()
+    whole = shard.gather_fold(crc, length)
+    exch = time.perf_counter() - t1
+    if rank == 0:
+        gs = golden_digests().get("single_record_seed0xc0de", {}).get("crc", {})
+        want = gs.get(str(world * n))
+        per = wall / args.steps
+        print(json.dumps({
+            "metric": "GiB/s CRC32C of one device-resident record split across GPUs "
+                      "(consus::crc32c semantics)",
+            "value": round(world * n / per / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: splitmix64 stream 0xC0DE, each rank's 4 GiB slice generated in "
+                    "its HBM",
+            "config": {"workload": f"1 x {world * 4} GiB record, 4 GiB slice per GPU, {world} x "
+                                   "MI355X; per-slice crc32c on each GPU, (crc, length) pairs "
+                                   "folded with crc32c_combine on rank 0",
+                       "parallelism": f"byte slices x{world}, 8-byte exchange after the timed "
+                                      "region"},
+            "roofline": {"bound": "hbm", "achieved": round(n / per / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(n / per / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "per-rank slice: crc32c_fixed_pipe_kernel + single_tree + "
+                                   "single_join (host sync included)"},
+            "exchange_ms": round(exch * 1e3, 3),
+            "digest_verified": (whole == want) if want is not None else None,
+            "crc": f"{whole:#010x}", "cpu_baseline": None}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -447,9 +504,9 @@ def main():
     # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.
     import consus_amd as E
     E.init(0 if args.share_device else local)
-    if args.config != "fixed4k":
+    if args.config != "fixed4k" and not (args.config == "single" and world > 1):
         if world != 1:
-            sys.exit("secondary configs run on one GPU")
+            sys.exit("secondary configs other than single run on one GPU")
         res = run_secondary(args, E, (traffic, traffic_note))
         if not args.child_pmc:
             print(json.dumps(res), flush=True)
@@ -469,6 +526,10 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
+
+    if args.config == "single":  # world > 1: one record split across the ranks
+        run_single_split(args, E, dist, rank, world)
+        return
 
     R, L = args.records_per_rank, args.record_bytes
     data = E.DeviceBuffer(R * L)

@@ -186,9 +186,10 @@ def main() -> None:
                       "into 64 MiB segments; digest = crc32c(0, LE CRC vector) per segment",
         "segments": segs}
     # one huge record (bench.py --config single): the whole
-    # first 4 GiB (and 4 GiB + 4097 B) of stream 0xC0DE as ONE crc32c
+    # first 4 GiB (and 4 GiB + 4097 B) of stream 0xC0DE as ONE crc32c; 8, 16
+    # and 32 GiB for the record split across 2, 4 and 8 GPUs
     single = {}
-    for nbytes in (1 << 32, (1 << 32) + 4097):
+    for nbytes in (1 << 32, (1 << 32) + 4097, 1 << 33, 1 << 34, 1 << 35):
         single[str(nbytes)] = ref.splitmix_stream(0xC0DE, 0, nbytes)
     digests["single_record_seed0xc0de"] = {
         "definition": "crc32c(0, bytes [0, n) of the splitmix64 stream 0xC0DE) as one record, "

@@ -404,3 +404,24 @@ def test_full_config2_zipf_golden(engine):
         assert engine.crc32c_device(out, R * 4) == g["digest"], hint
     for b in (data, d_off, d_len, out):
         b.free()
+
+
+def test_split_record_fold_golden(engine):
+    """One 4 GiB record split into 2..8 slices as if over 2..8 GPUs (here
+    all on one): per-slice device CRCs folded with crc32c_combine equal the
+    golden CRC of the whole record, with and without an init."""
+    from consus_amd import shard
+    gold = _gold("single_record_seed0xc0de")["crc"]
+    n = 1 << 32
+    data = engine.DeviceBuffer(n)
+    data.fill_splitmix64(0xC0DE)
+    for world in (2, 3, 8):
+        sl = shard.record_slices(n, world)
+        crcs = [engine.crc32c_device(data, L, offset=s) for s, L in sl]
+        assert shard.fold_slice_crcs(crcs, [L for _, L in sl]) == gold[str(n)]
+    init = 0x9E3779B9
+    sl = shard.record_slices(n, 4, align=1 << 20)
+    crcs = [engine.crc32c_device(data, L, offset=s) for s, L in sl]
+    assert shard.fold_slice_crcs(crcs, [L for _, L in sl], init) == \
+        engine.crc32c_device(data, n, init_crc=init)
+    data.free()

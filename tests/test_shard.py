@@ -74,3 +74,56 @@ def test_two_rank_gloo_digest_gather(tmp_path):
     mp.spawn(_worker, args=(2, port, str(out)), nprocs=2, join=True)
     r = json.load(open(out))
     assert r["combined"] == r["full"]
+
+
+def test_record_slices_cover():
+    for n in (0, 1, 4095, 4096 * 8 - 1, 4096 * 8, 10**7 + 3):
+        for world in (1, 2, 3, 8):
+            sl = shard.record_slices(n, world)
+            assert len(sl) == world and sl[0][0] == 0
+            assert all(a[0] + a[1] == b[0] for a, b in zip(sl, sl[1:]))
+            assert sl[-1][0] + sl[-1][1] == n
+            assert all(s % 4096 == 0 for s, _ in sl)
+
+
+def test_fold_slice_crcs_matches_whole_record(oracle):
+    """One record split over 1..8 ranks: the fold of the per-slice CRCs
+    equals crc32c(init, record) from the oracle, empty slices included."""
+    rng = np.random.default_rng(7)
+    for n in (0, 100, 4096 * 3 + 5, 200000):
+        buf = rng.integers(0, 256, n, dtype=np.uint8)
+        for world in (1, 2, 3, 8):
+            for init in (0, int(rng.integers(0, 2**32))):
+                sl = shard.record_slices(n, world, align=4096)
+                crcs = [oracle.crc32c(0, buf[s:s + L]) for s, L in sl]
+                assert shard.fold_slice_crcs(crcs, [L for _, L in sl], init) == \
+                    oracle.crc32c(init, buf)
+
+
+def _split_worker(rank, world, port, result_path):
+    import torch.distributed as dist
+    from oracle.oracle import Oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    orc = Oracle()
+    n = 3 * 4096 * 5 + 777
+    data = orc.fill(n, 0xC0DE, 0)
+    s, L = shard.record_slices(n, world)[rank]
+    got = shard.gather_fold(orc.crc32c(0, data[s:s + L]), L, init=0x1234ABCD)
+    if rank == 0:
+        with open(result_path, "w") as f:
+            json.dump({"folded": got, "whole": orc.crc32c(0x1234ABCD, data)}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_split_record(tmp_path):
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = tmp_path / "split.json"
+    mp.spawn(_split_worker, args=(2, port, str(out)), nprocs=2, join=True)
+    r = json.load(open(out))
+    assert r["folded"] == r["whole"]
