@@ -69,7 +69,10 @@ def parse():
                          "at N > 1 one N x 4 GiB record split across the GPUs, SURVEY 8(e)); "
                          "dlog = the durable-log front-end (SURVEY 8(f)1): appends/s of 8 "
                          "threads, GPU batch CRC per flushed segment")
-    ap.add_argument("--segments", type=int, default=16, help="stream/pcie4k: segments per step")
+    ap.add_argument("--segments", type=int, default=None,
+                    help="stream/pcie4k: 64 MiB segments per step (default 16 for stream; 64 for "
+                         "pcie4k = the whole 1M-record configs[1] batch, checked against its "
+                         "golden block digest)")
     ap.add_argument("--records-per-rank", type=int, default=None,
                     help="default: 1M (configs[1]) on one GPU, 2M per GPU when N > 1, so that "
                          "N = 8 is configs[3] (16M x 4 KiB across 8 GPUs)")
@@ -346,7 +349,7 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
             "digest_verified": ok, "crc": f"{got:#010x}"})
         return res
     # stream / pcie4k: host-resident segments through the H2D -> CRC -> D2H pipeline
-    nseg = args.segments
+    nseg = args.segments or (64 if args.config == "pcie4k" else 16)
     filler = E.DeviceBuffer(W.SEGMENT_BYTES + 64)
 
     def fill(nbytes, byte_off, seed):

@@ -36,4 +36,6 @@ stats zipf
 stats single
 run bench_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --share-device --steps 5 --warmup 2 --no-cpu
+run bench_single_split_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --config single --share-device --steps 10 --warmup 2
 echo "ALL OK"

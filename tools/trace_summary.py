@@ -1,0 +1,33 @@
+"""Summarise the headline kernel's dispatches from a rocprofv3 kernel trace
+and set them beside bench.py's in-run HIP-event launch time (dev tool).
+
+python tools/trace_summary.py gpurun_out/prof_r01 > profiles/r01_fixed4k_kernel_trace_summary.txt
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+d = sys.argv[1]
+rows = [r for r in csv.DictReader(open(os.path.join(d, "rocprof_fixed4k", "k_kernel_trace.csv")))
+        if "crc32c_fixed_pipe_kernel<4, false>" in r["Kernel_Name"]]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+big = [u for u, r in zip(us, rows) if int(r["Grid_Size_X"]) >= 256 * 1024 and u > 100]
+small = [u for u in us if u <= 100]
+bench = {}
+for line in open(os.path.join(d, "rocprof_fixed4k.log")):
+    if line.startswith("{"):
+        bench = json.loads(line)
+print("# rocprofv3 --kernel-trace of: bench.py --config fixed4k --no-cpu --no-pmc --steps 30 --warmup 5")
+print(f"# crc32c_fixed_pipe_kernel<4, false>: {len(us)} dispatches = {len(big)} over the 1M x 4 KiB "
+      f"batch\n# (5 warmup + 30 timed) + {len(small)} over the 4 MiB CRC vector (the digest check "
+      f"after timing,\n# same kernel through launch_single), which pulls the stats-file average down.")
+print(f"1M x 4 KiB dispatches: n={len(big)} mean={statistics.mean(big):.1f} us "
+      f"median={statistics.median(big):.1f} us min={min(big):.1f} us max={max(big):.1f} us")
+t = big[-30:]
+print(f"timed 30 (last 30): mean={statistics.mean(t):.1f} us  -> bench.py in-run HIP events: "
+      f"launch_ms {bench.get('roofline', {}).get('launch_ms')}")
+if small:
+    print(f"digest dispatches: {statistics.mean(small):.1f} us")
