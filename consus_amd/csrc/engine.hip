@@ -327,7 +327,6 @@ int run_fixed(DeviceState* d, Ctx* c, const void* base, uint64_t stride, uint64_
                              d->cus, c->stream));
         return MI_CRC32C_OK;
     }
-    if (length > 0xFFFFFFFFull) return fail(MI_CRC32C_EINVAL, "fixed length >= 4 GiB");
     int st;
     if ((st = c->off.reserve(count * 8)) || (st = c->len.reserve(count * 4))) return st;
     HIP_TRY(launch_make_fixed_records(c->off.as<uint64_t>(), c->len.as<uint32_t>(), count, stride,
@@ -402,6 +401,8 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
     for (size_t i = 0; i < count; ++i)
     {
         if (lengths[i] == 0) continue;
+        if (offsets[i] > UINT64_MAX - lengths[i])
+            return fail(MI_CRC32C_EINVAL, "record end overflows 64 bits");
         lo = std::min<uint64_t>(lo, offsets[i]);
         hi = std::max<uint64_t>(hi, offsets[i] + lengths[i]);
         total += lengths[i];
@@ -436,6 +437,11 @@ int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
 {
     if (count == 0) return MI_CRC32C_OK;
     if (!out || (!base && length)) return fail(MI_CRC32C_EINVAL, "null pointer with count > 0");
+    if (length > 0xFFFFFFFFull) return fail(MI_CRC32C_EINVAL, "fixed length >= 4 GiB");
+    uint64_t span = 0;  // bytes from the first record's start to the last one's end
+    if (length && (__builtin_mul_overflow(uint64_t(count - 1), stride, &span) ||
+                   __builtin_add_overflow(span, length, &span)))
+        return fail(MI_CRC32C_EINVAL, "batch span overflows 64 bits");
     int st = 0;
     Ctx* c = thread_ctx(&st);
     if (!c) return st;
@@ -445,7 +451,6 @@ int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
         if ((st = run_fixed(d, c, base, stride, length, inits, count, out))) return st;
         return finish(c, flags);
     }
-    const uint64_t span = length ? (count - 1) * stride + length : 0;
     if ((st = c->data.reserve(span + 16)) || (st = c->out.reserve(count * 4)) ||
         (inits && (st = c->inits.reserve(count * 4))))
         return st;
@@ -680,22 +685,24 @@ int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, s
                               const uint32_t* inits, size_t count, uint32_t* host_out,
                               uint64_t* ticket)
 {
-    if (!p || bytes > p->max_bytes || count > p->max_records || (count && (!offsets || !lengths)))
-        return fail(MI_CRC32C_EINVAL, "segment exceeds pipeline limits");
+    if (!p || bytes > p->max_bytes || count > p->max_records || (count && (!offsets || !lengths)) ||
+        (bytes && !host_segment) || (count && !host_out))
+        return fail(MI_CRC32C_EINVAL, "segment exceeds pipeline limits or null pointer");
+    // validated before a ticket is taken: a refused segment leaves no trace
+    uint64_t total = 0, maxlen = 0;
+    for (size_t i = 0; i < count; ++i)
+    {
+        if (lengths[i] && (offsets[i] > bytes || lengths[i] > bytes - offsets[i]))
+            return fail(MI_CRC32C_EINVAL, "record outside segment");
+        total += lengths[i];
+        maxlen = std::max<uint64_t>(maxlen, lengths[i]);
+    }
     std::lock_guard<std::mutex> lock(p->mu);
     DeviceState* d = g_dev.load();
     const uint64_t t = p->next_ticket++;
     auto& s = p->slots[t % p->slots.size()];
     int st;
     if ((st = slot_complete(s))) return st;
-    uint64_t total = 0, maxlen = 0;
-    for (size_t i = 0; i < count; ++i)
-    {
-        if (lengths[i] && offsets[i] + lengths[i] > bytes)
-            return fail(MI_CRC32C_EINVAL, "record outside segment");
-        total += lengths[i];
-        maxlen = std::max<uint64_t>(maxlen, lengths[i]);
-    }
     const void* src = host_segment;
     if (bytes && !is_pinned(host_segment))
     {

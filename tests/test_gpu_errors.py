@@ -1,0 +1,108 @@
+"""Error behaviour of the C ABI on a live device (include/consus_crc32c.h):
+bad arguments return MI_CRC32C_EINVAL with a message in
+mi_crc32c_last_error(), nothing is launched, and the engine keeps working
+for the next valid call.  The reference function has no error channel
+(common/crc32c.h:40-41); these are the status codes of the batch ABI."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def L(engine):
+    return engine.lib()
+
+
+def _u32(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _still_works(engine):
+    assert engine.crc32c(0, b"123456789") == 0xE3069283
+
+
+def _einval(engine, L, st):
+    assert st == engine.EINVAL
+    assert L.mi_crc32c_last_error()  # a message, not empty
+    _still_works(engine)
+
+
+def test_strerror_names_every_status(L, engine):
+    for st in (0, engine.EINVAL, engine.ENODEV, -12, -5, -71):
+        assert L.mi_crc32c_strerror(st)
+
+
+def test_batch_argument_errors(L, engine):
+    out = np.zeros(4, dtype=np.uint32)
+    off = np.zeros(4, dtype=np.uint64)
+    ln = np.full(4, 8, dtype=np.uint32)
+    buf = np.zeros(64, dtype=np.uint8)
+    # count == 0 is a no-op whatever the pointers
+    assert L.mi_crc32c_batch(None, None, None, None, 0, 0, None, 0) == 0
+    _einval(engine, L, L.mi_crc32c_batch(_u32(buf), None, _u32(ln), None, 4, 0, _u32(out), 0))
+    _einval(engine, L, L.mi_crc32c_batch(_u32(buf), _u32(off), _u32(ln), None, 4, 0, None, 0))
+    _einval(engine, L, L.mi_crc32c_batch(None, _u32(off), _u32(ln), None, 4, 0, _u32(out), 0))
+    # a record whose end wraps the 64-bit address space
+    bad = np.array([2**64 - 4], dtype=np.uint64)
+    _einval(engine, L, L.mi_crc32c_batch(_u32(buf), _u32(bad), _u32(ln[:1]), None, 1, 0,
+                                         _u32(out), 0))
+    _einval(engine, L, L.mi_crc32c_batch_fixed(_u32(buf), 16, 8, None, 4, None, 0))
+    _einval(engine, L, L.mi_crc32c_batch_fixed(None, 16, 8, None, 4, _u32(out), 0))
+    _einval(engine, L, L.mi_crc32c_batch_fixed(_u32(buf), 16, 1 << 32, None, 2, _u32(out), 0))
+
+
+def test_buffer_argument_errors(L, engine):
+    o = C.c_uint32(7)
+    _einval(engine, L, L.mi_crc32c_buffer(0, None, 0, None, 0))
+    _einval(engine, L, L.mi_crc32c_buffer(0, None, 5, C.byref(o), 0))
+    assert L.mi_crc32c_buffer(0xABCD, None, 0, C.byref(o), 0) == 0 and o.value == 0xABCD
+    z = np.zeros(4, dtype=np.uint32)
+    _einval(engine, L, L.mi_crc32c_combine_batch(None, _u32(z), _u32(z), 4, _u32(z), 0))
+
+
+def test_pipeline_argument_errors(L, engine):
+    p = C.c_void_p()
+    _einval(engine, L, L.mi_crc32c_pipeline_create(1 << 20, 0, 2, C.byref(p)))
+    _einval(engine, L, L.mi_crc32c_pipeline_create(1 << 20, 16, 0, C.byref(p)))
+    assert L.mi_crc32c_pipeline_create(1 << 20, 16, 2, C.byref(p)) == 0
+    try:
+        seg = np.arange(4096, dtype=np.uint8)
+        off = np.array([0, 100], dtype=np.uint64)
+        ln = np.array([100, 200], dtype=np.uint32)
+        out = np.zeros(2, dtype=np.uint32)
+        t = C.c_uint64()
+        # larger than the pipeline's segment limit
+        big = np.zeros((1 << 20) + 1, dtype=np.uint8)
+        _einval(engine, L, L.mi_crc32c_pipeline_submit(p, _u32(big), big.size, _u32(off),
+                                                       _u32(ln), None, 2, _u32(out), C.byref(t)))
+        # a record past the segment end, and one whose end wraps 64 bits
+        for o2 in (4000, 2**64 - 50):
+            off2 = np.array([0, o2], dtype=np.uint64)
+            _einval(engine, L, L.mi_crc32c_pipeline_submit(p, _u32(seg), seg.size, _u32(off2),
+                                                           _u32(ln), None, 2, _u32(out),
+                                                           C.byref(t)))
+        _einval(engine, L, L.mi_crc32c_pipeline_submit(p, None, seg.size, _u32(off), _u32(ln),
+                                                       None, 2, _u32(out), C.byref(t)))
+        # refused submits took no ticket: the next good one completes normally
+        assert L.mi_crc32c_pipeline_submit(p, _u32(seg), seg.size, _u32(off), _u32(ln), None, 2,
+                                           _u32(out), C.byref(t)) == 0
+        assert L.mi_crc32c_pipeline_wait(p, t.value) == 0
+        assert list(out) == [engine.crc32c(0, seg[0:100]), engine.crc32c(0, seg[100:300])]
+    finally:
+        assert L.mi_crc32c_pipeline_destroy(p) == 0
+
+
+def test_device_helper_errors(L, engine):
+    buf = engine.DeviceBuffer(4096)
+    _einval(engine, L, L.mi_fill_splitmix64(C.c_void_p(buf.ptr + 3), 64, 1, 0))
+    _einval(engine, L, L.mi_fill_splitmix64(C.c_void_p(buf.ptr), 64, 1, 5))
+    recv = engine.DeviceBuffer(4096)
+    _einval(engine, L, L.mi_comm_allgather_u32(C.c_void_p(buf.ptr), 16, C.c_void_p(recv.ptr)))
+    # a second device while the engine is bound to device 0
+    assert L.mi_crc32c_init(1) != 0
+    _still_works(engine)
+    buf.free()
+    recv.free()
