@@ -713,10 +713,23 @@ extern "C" {
 
 mi_dlog* mi_dlog_create(size_t segment_capacity) { return new mi_dlog(segment_capacity); }
 void mi_dlog_destroy(mi_dlog* l) { delete l; }
-int mi_dlog_open(mi_dlog* l, const char* dir) { return l->log.open(dir) ? 1 : 0; }
+int mi_dlog_open(mi_dlog* l, const char* dir)
+{
+    if (!l || !dir)
+    {
+        errno = EINVAL;
+        return 0;
+    }
+    return l->log.open(dir) ? 1 : 0;
+}
 void mi_dlog_close(mi_dlog* l) { l->log.close(); }
 int64_t mi_dlog_append(mi_dlog* l, const void* entry, size_t sz)
 {
+    if (!l || (!entry && sz))
+    {
+        errno = EINVAL;
+        return -1;
+    }
     return l->log.append(static_cast<const unsigned char*>(entry), sz);
 }
 int64_t mi_dlog_durable(mi_dlog* l) { return l->log.durable(); }

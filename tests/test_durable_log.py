@@ -222,3 +222,22 @@ def test_concurrent_appenders_full_segments(make_log, tmp_path, capacity):
     assert log.frames_flushed() == 3200
     log.close()
     assert log.replay() == [got[i] for i in range(1, 3201)]
+
+
+def test_c_abi_refuses_null_arguments(make_log, tmp_path):
+    """The C ABI refuses a null entry with a size and a null directory
+    (-1 / 0 with errno EINVAL) instead of dereferencing them; the log keeps
+    working."""
+    from consus_amd.durable_log import _lib
+    log = make_log()
+    assert _lib().mi_dlog_open(log._h, None) == 0
+    assert log.open(str(tmp_path))
+    assert _lib().mi_dlog_append(log._h, None, 5) == -1
+    assert _lib().mi_dlog_append(log._h, None, 0) == 1  # an empty entry is valid
+    r = log.append(b"after")
+    assert r == 2
+    wait_durable(log, r)
+    log.close()
+    frames = parse_frames(os.path.join(str(tmp_path), "file_a")) + \
+        parse_frames(os.path.join(str(tmp_path), "file_b"))
+    assert sorted((f[0], f[1]) for f in frames) == [(1, b""), (2, b"after")]
