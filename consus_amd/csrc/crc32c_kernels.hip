@@ -416,7 +416,8 @@ constexpr uint32_t kPlanPer = MI_PLAN_PER;
 constexpr uint32_t kPlanRecs = kPlanThreads * kPlanPer;
 constexpr uint32_t kHdrTotal = kPlanHdrTotal;
 constexpr uint32_t kHdrLongs = kBins + 1;
-static_assert(kHdrLongs < kPlanHdrWords, "plan header size");
+constexpr uint32_t kHdrGrab = kBins + 2;  // chunk kernel's shared-pool cursor
+static_assert(kHdrGrab < kPlanHdrWords, "plan header size");
 
 uint32_t var_plan_blocks(uint64_t count)
 {
@@ -560,7 +561,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_count_kernel(
         uint32_t bc[kBins];
         unpack_counts(t, bc);
         for (uint32_t b = 0; b < kBins; ++b) blk[b * nblocks + blockIdx.x] = bc[b];
-        if (blockIdx.x == 0) plan_hdr_d(blk, nblocks)[kHdrLongs] = 0;  // plan_scatter appends
+        if (blockIdx.x == 0)
+        {
+            plan_hdr_d(blk, nblocks)[kHdrLongs] = 0;      // plan_scatter appends
+            plan_hdr_d(blk, nblocks)[kHdrGrab] = 0;       // chunk kernel pool cursor
+        }
     }
 }
 
@@ -939,18 +944,26 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
 // want as many waves as possible; run one after the other they cost the sum
 // of the two, run side by side on every CU (4 "lead" waves on the 4-group
 // pieces, 12 on the rest) they overlap.  A batch with only one kind gives
-// every wave to it.  Item assignment is static: a global work queue would
-// need one atomic per grab on a single address, which serialised
-// (~12 ns/atomic chip-wide) into a 2x slower step when tried.
+// every wave to it.  Item assignment is static except for a tail pool of
+// 4-group pieces that waves of both roles drain when their own share is done,
+// one atomic per 128-piece wave grab: a queue with one atomic per piece on a
+// single address serialised (~12 ns/atomic chip-wide) into a 2x slower step.
 constexpr uint32_t kLeadWaves = 4;
 constexpr uint32_t kLeadAuto = ~0u;  // lead_override: pick from the plan (any value > 16)
 
+// Shared pool (cfg 3, MI355X, same-box A/B): the last 30 % of the 4-group
+// pieces, grabbed 128 at a time (16 per team): 0.892-0.896 ms per step
+// against 0.904-0.929 with every piece statically assigned; 15-50 % pools
+// and 32/64-piece grabs gain less, 256-piece grabs lose (coarse tail).
+constexpr uint32_t kShareFrac = 30;  // % of the 4-group pieces in the shared pool
+constexpr uint32_t kGrab = 128;      // pool pieces per wave grab
+
 __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
-    const Item* __restrict__ items, const uint32_t* __restrict__ blk, uint32_t nblocks,
+    const Item* __restrict__ items, uint32_t* __restrict__ blk, uint32_t nblocks,
     uint32_t* __restrict__ partial, uint64_t item_cap, const uint32_t* __restrict__ tables,
     uint32_t lead_override)
 {
-    const uint32_t* hdr = blk + kBins * nblocks;  // plan_hdr
+    uint32_t* hdr = blk + kBins * nblocks;  // plan_hdr
     const uint32_t n_items = hdr[kHdrTotal];
     if (n_items > item_cap || n_items == 0) return;
     // bins: [hdr[0], hdr[1]) 4 groups, [hdr[1], hdr[2]) 3, [hdr[2], hdr[3]) 2,
@@ -966,11 +979,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
     const uint32_t tw = (threadIdx.x & 63u) / kTeam;
     const uint32_t li = lane_info();
     const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
+    // With both roles present, the last kShareFrac % of the 4-group pieces
+    // form a pool that every wave drains once its static share is done, so
+    // neither role idles while the other finishes.
+    const bool mixed = lead != 0 && lead != 16;
+    const uint32_t split = mixed ? b1 - uint32_t(uint64_t(b1 - b0) * kShareFrac / 100u) : b1;
     if (wave < lead)
     {
         const uint32_t team = (blockIdx.x * lead + wave) * kTeam + tw;
         const uint32_t nteams = gridDim.x * lead * kTeam;
-        chunk_bin<4>(items, b0, b1, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin<4>(items, b0, split, partial, team, team & ~7u, nteams, tl, li, zero16);
     }
     else
     {
@@ -980,6 +998,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
         chunk_bin<3>(items, b1, b2, partial, team, team & ~7u, nteams, tl, li, zero16);
         chunk_bin<2>(items, b2, b3, partial, team, team & ~7u, nteams, tl, li, zero16);
         chunk_bin<1>(items, b3, n_items, partial, team, team & ~7u, nteams, tl, li, zero16);
+    }
+    // one relaxed atomic per wave grab; every wave leaves once the pool is empty
+    while (split < b1)
+    {
+        uint32_t got = 0;
+        if ((threadIdx.x & 63u) == 0)
+            got = __hip_atomic_fetch_add(hdr + kHdrGrab, kGrab, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t lo = split + __builtin_amdgcn_readfirstlane(got);
+        if (lo >= b1) break;
+        chunk_bin<4>(items, lo, min(lo + kGrab, b1), partial, tw, 0u, 64u / kTeam, tl, li, zero16);
     }
 }
 
