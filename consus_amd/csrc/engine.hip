@@ -180,6 +180,12 @@ struct DevBuf
         cap = want;
         return MI_CRC32C_OK;
     }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
     template <typename T>
     T* as() const { return static_cast<T*>(p); }
 };
@@ -202,6 +208,12 @@ struct PinBuf
     }
     template <typename T>
     T* as() const { return static_cast<T*>(p); }
+    void release()
+    {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
 };
 
 // Per-(thread or pipeline slot) execution context.
@@ -222,23 +234,56 @@ struct Ctx
         HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         return pin_small.reserve(4096);
     }
+    // Waits for the stream's work, then frees every buffer, event and the stream.
+    void release()
+    {
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
+                          &last_pos, &blk, &longs})
+            b->release();
+        pin_small.release();
+        for (hipEvent_t* e : {&ev0, &ev1, &done})
+            if (*e)
+            {
+                (void)hipEventDestroy(*e);
+                *e = nullptr;
+            }
+        if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
 };
 
-thread_local Ctx* t_ctx = nullptr;
+// One context per calling thread, released when the thread exits (a durable
+// log's flush thread lives as long as the log is open; its workspaces go
+// with it).
+struct ThreadCtx
+{
+    Ctx* c = nullptr;
+    ~ThreadCtx()
+    {
+        if (c)
+        {
+            c->release();
+            delete c;
+        }
+    }
+};
+thread_local ThreadCtx t_ctx;
 
 Ctx* thread_ctx(int* status)
 {
     DeviceState* d = dev_or_init(status);
     if (!d) return nullptr;
-    if (t_ctx) return t_ctx;
-    auto* c = new Ctx;  // per-thread, never freed (threads are few and long-lived)
+    if (t_ctx.c) return t_ctx.c;
+    auto* c = new Ctx;
     *status = c->open(d->ordinal);
     if (*status != MI_CRC32C_OK)
     {
+        c->release();
         delete c;
         return nullptr;
     }
-    t_ctx = c;
+    t_ctx.c = c;
     return c;
 }
 
@@ -747,21 +792,10 @@ int mi_crc32c_pipeline_destroy(mi_crc32c_pipeline* p)
     int rc = MI_CRC32C_OK;
     for (auto& s : p->slots)
     {
-        if (s.ctx.stream)
-        {
-            if (s.ticket) rc = slot_complete(s);
-            (void)hipStreamSynchronize(s.ctx.stream);
-        }
-        for (DevBuf* b : {&s.ctx.data, &s.ctx.off, &s.ctx.len, &s.ctx.inits, &s.ctx.out,
-                          &s.ctx.items, &s.ctx.partial, &s.ctx.first_pos, &s.ctx.int_pos,
-                          &s.ctx.last_pos, &s.ctx.blk, &s.ctx.longs, &s.dseg, &s.dmeta})
-            if (b->p) (void)hipFree(b->p);
-        for (PinBuf* b : {&s.ctx.pin_small, &s.seg, &s.meta, &s.res})
-            if (b->p) (void)hipHostFree(b->p);
-        if (s.ctx.ev0) (void)hipEventDestroy(s.ctx.ev0);
-        if (s.ctx.ev1) (void)hipEventDestroy(s.ctx.ev1);
-        if (s.ctx.done) (void)hipEventDestroy(s.ctx.done);
-        if (s.ctx.stream) (void)hipStreamDestroy(s.ctx.stream);
+        if (s.ctx.stream && s.ticket) rc = slot_complete(s);
+        s.ctx.release();
+        for (DevBuf* b : {&s.dseg, &s.dmeta}) b->release();
+        for (PinBuf* b : {&s.seg, &s.meta, &s.res}) b->release();
     }
     delete p;
     return rc;

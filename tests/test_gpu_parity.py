@@ -425,3 +425,31 @@ def test_split_record_fold_golden(engine):
     assert shard.fold_slice_crcs(crcs, [L for _, L in sl], init) == \
         engine.crc32c_device(data, n, init_crc=init)
     data.free()
+
+
+def test_short_lived_threads_release_contexts(engine, oracle):
+    """Each calling thread gets its own stream and workspaces, released when
+    the thread exits: 48 threads in turn, each with host and device batches
+    (workspaces grown to several MiB), then the calling thread again."""
+    import threading
+    rng = np.random.default_rng(77)
+    lengths = rng.integers(0, 70000, 300).astype(np.uint32)
+    offsets = np.zeros(lengths.size, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    buf = rng.integers(0, 256, int(lengths.sum()) + 64, dtype=np.uint8)
+    want = oracle.batch(buf, offsets, lengths)
+    errors = []
+
+    def work():
+        try:
+            assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, planned=True), want)
+            assert engine.crc32c(0, buf[:100000]) == oracle.crc32c(0, buf[:100000])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    for _ in range(48):
+        t = threading.Thread(target=work)
+        t.start()
+        t.join()
+    assert not errors, errors[0]
+    work()
+    assert not errors
