@@ -453,3 +453,19 @@ def test_short_lived_threads_release_contexts(engine, oracle):
     assert not errors, errors[0]
     work()
     assert not errors
+
+
+def test_config1_golden(engine):
+    """BASELINE configs[0] (1K x 256 B records, the reference's CPU case)
+    through the GPU: one fixed-stride host batch and per-record drop-in
+    calls, against the CRCs the compiled reference produced."""
+    import base64
+    g = _gold("cfg1_fixed_256_seed0x1_1024")
+    want = np.frombuffer(base64.b64decode(g["crcs_b64_le_u32"]), dtype="<u4")
+    data = engine.DeviceBuffer(1024 * 256)
+    data.fill_splitmix64(1)
+    host = data.download(np.uint8)
+    assert np.array_equal(engine.crc32c_fixed(host, 256, 256, 1024), want)
+    for i in range(0, 1024, 97):
+        assert engine.crc32c(0, host[256 * i:256 * (i + 1)]) == int(want[i])
+    data.free()
