@@ -469,3 +469,32 @@ def test_config1_golden(engine):
     for i in range(0, 1024, 97):
         assert engine.crc32c(0, host[256 * i:256 * (i + 1)]) == int(want[i])
     data.free()
+
+
+def test_config4_log_segments_golden(engine):
+    """BASELINE configs[4]: real durable-log frames packed into 64 MiB
+    segments, through the streaming pipeline (H2D + CRC + D2H), each
+    segment's CRC vector digested against the reference's golden digest."""
+    from consus_amd import workload as W
+    gold = _gold("log_segments_64MiB")["segments"][:2]
+    filler = engine.DeviceBuffer(W.SEGMENT_BYTES + 64)
+
+    def fill(nbytes, byte_off):
+        a = byte_off & ~7
+        n = nbytes + (byte_off - a)
+        filler.fill_splitmix64(W.DATA_SEED, byte_offset=a, nbytes=(n + 7) & ~7)
+        return filler.download(np.uint8, n)[byte_off - a:]
+    pipe = engine.Pipeline(W.SEGMENT_BYTES, 20000, depth=2)
+    dev = engine.DeviceBuffer(20000 * 4)
+    try:
+        for (buf, fo, fl), g in zip(W.log_segments(len(gold), fill), gold):
+            assert fo.size == g["frames"] and buf.size == g["bytes"]
+            out = np.zeros(fo.size, dtype=np.uint32)
+            pipe.wait(pipe.submit(buf, fo, fl, out))
+            assert int(out[0]) == g["first_crc"]
+            dev.upload(out)
+            assert engine.crc32c_device(dev, out.size * 4) == g["digest"]
+    finally:
+        pipe.close()
+        dev.free()
+        filler.free()
