@@ -45,6 +45,9 @@ int fail(int status, const std::string& msg)
             return fail(MI_CRC32C_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// Host batches whose packed inputs fit this take one staging copy.
+constexpr uint64_t kPackMax = uint64_t(4) << 20;
+constexpr uint64_t kPackInPlace = uint64_t(512) << 10;
 // Device buffers from this size take launch_single (fixed-record kernel on
 // the 4 KiB chunks + a two-level combine tree) instead of the variable path.
 constexpr uint64_t kSingleMin = 64 * 1024;
@@ -224,6 +227,7 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     PinBuf pin_small;                   // plan-size read-back, small host outputs
+    PinBuf pin_stage, pin_out;          // packed small host batches: inputs, CRCs
 
     int open(int ordinal)
     {
@@ -241,7 +245,7 @@ struct Ctx
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs})
             b->release();
-        pin_small.release();
+        for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
             if (*e)
             {
@@ -285,6 +289,17 @@ Ctx* thread_ctx(int* status)
     }
     t_ctx.c = c;
     return c;
+}
+
+bool is_pinned(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
 }
 
 uint32_t apply_zeros(const DeviceState* d, uint32_t s, uint64_t n)
@@ -455,6 +470,53 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
     }
     if (lo == UINT64_MAX) lo = hi = 0;
     if (hi > lo && !base) return fail(MI_CRC32C_EINVAL, "null base");
+    const uint64_t maxlen_arg = (flags & MI_CRC32C_PLANNED) ? UINT64_MAX : maxlen;
+    // Small batches (a consus::crc32c call, a durable-log flush): offsets,
+    // lengths, inits -- and the bytes, unless they already sit in pinned
+    // memory -- packed into one pinned staging buffer and moved with ONE
+    // copy; the CRCs come back into pinned memory.  Each pageable
+    // hipMemcpyAsync costs a staging round trip of its own.
+    const uint64_t meta = uint64_t(count) * (inits ? 16 : 12);
+    // bytes already pinned are DMA'd in place only when large: below ~512 KiB a
+    // CPU copy into the packed buffer beats a second copy command (measured:
+    // 400 frames, 227 KB: 50 us packed vs 54 us with the bytes DMA'd in place)
+    const bool src_pinned = hi - lo > kPackInPlace &&
+                            is_pinned(static_cast<const uint8_t*>(base) + lo);
+    const uint64_t data_at = (meta + 127) & ~uint64_t(127);
+    const uint64_t packed = data_at + (src_pinned ? 0 : hi - lo);
+    if (packed <= kPackMax)
+    {
+        if ((st = c->pin_stage.reserve(packed + 16)) || (st = c->pin_out.reserve(count * 4)) ||
+            (st = c->off.reserve(packed + 16)) || (st = c->out.reserve(count * 4)) ||
+            (src_pinned && (st = c->data.reserve(hi - lo + 16))))
+            return st;
+        uint8_t* hp = c->pin_stage.as<uint8_t>();
+        uint64_t* ho = reinterpret_cast<uint64_t*>(hp);
+        for (size_t i = 0; i < count; ++i) ho[i] = lengths[i] ? offsets[i] - lo : 0;
+        std::memcpy(hp + count * 8, lengths, count * 4);
+        if (inits) std::memcpy(hp + count * 12, inits, count * 4);
+        if (!src_pinned && hi > lo)
+            std::memcpy(hp + data_at, static_cast<const uint8_t*>(base) + lo, hi - lo);
+        uint8_t* dp = c->off.as<uint8_t>();
+        HIP_TRY(hipMemcpyAsync(dp, hp, packed, hipMemcpyHostToDevice, c->stream));
+        const uint8_t* dbase = dp + data_at;
+        if (src_pinned)
+        {
+            HIP_TRY(hipMemcpyAsync(c->data.p, static_cast<const uint8_t*>(base) + lo, hi - lo,
+                                   hipMemcpyHostToDevice, c->stream));
+            dbase = c->data.as<uint8_t>();
+        }
+        if ((st = run_var(d, c, dbase, reinterpret_cast<const uint64_t*>(dp),
+                          reinterpret_cast<const uint32_t*>(dp + count * 8),
+                          inits ? reinterpret_cast<const uint32_t*>(dp + count * 12) : nullptr,
+                          count, total, c->out.as<uint32_t>(), maxlen_arg)))
+            return st;
+        HIP_TRY(hipMemcpyAsync(c->pin_out.p, c->out.p, count * 4, hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        std::memcpy(out, c->pin_out.p, count * 4);
+        return MI_CRC32C_OK;
+    }
     std::vector<uint64_t> reb(count);
     for (size_t i = 0; i < count; ++i) reb[i] = lengths[i] ? offsets[i] - lo : 0;
     if ((st = c->data.reserve(hi - lo + 16)) || (st = c->off.reserve(count * 8)) ||
@@ -470,7 +532,7 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
         HIP_TRY(hipMemcpyAsync(c->inits.p, inits, count * 4, hipMemcpyHostToDevice, c->stream));
     if ((st = run_var(d, c, c->data.p, c->off.as<uint64_t>(), c->len.as<uint32_t>(),
                       inits ? c->inits.as<uint32_t>() : nullptr, count, total,
-                      c->out.as<uint32_t>(), (flags & MI_CRC32C_PLANNED) ? UINT64_MAX : maxlen)))
+                      c->out.as<uint32_t>(), maxlen_arg)))
         return st;
     HIP_TRY(hipMemcpyAsync(out, c->out.p, count * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -683,16 +745,6 @@ int slot_complete(mi_crc32c_pipeline::Slot& s)
     return MI_CRC32C_OK;
 }
 
-bool is_pinned(const void* p)
-{
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess)
-    {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeHost;
-}
 
 }  // namespace
 
