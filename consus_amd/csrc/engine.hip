@@ -48,6 +48,7 @@ int fail(int status, const std::string& msg)
 // Host batches whose packed inputs fit this take one staging copy.
 constexpr uint64_t kPackMax = uint64_t(4) << 20;
 constexpr uint64_t kPackInPlace = uint64_t(512) << 10;
+constexpr uint64_t kZeroCopyMax = uint64_t(8) << 10;  // packed inputs read in place by the GPU
 // Device buffers from this size take launch_single (fixed-record kernel on
 // the 4 KiB chunks + a two-level combine tree) instead of the variable path.
 constexpr uint64_t kSingleMin = 64 * 1024;
@@ -196,16 +197,23 @@ struct DevBuf
 struct PinBuf
 {
     void* p = nullptr;
+    void* dev = nullptr;  // the device's address of the same bytes (mapped pinned memory)
     size_t cap = 0;
     int reserve(size_t bytes)
     {
         if (bytes <= cap) return MI_CRC32C_OK;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         size_t want = std::max<size_t>(bytes, 4096);
-        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&p, want, hipHostMallocMapped) != hipSuccess)
+        {
+            p = nullptr;
             return fail(MI_CRC32C_ENOMEM, "hipHostMalloc(" + std::to_string(want) + ") failed");
+        }
+        if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess)
+        {
+            (void)hipGetLastError();
+            dev = nullptr;  // no device mapping: callers stage through a copy
+        }
         cap = want;
         return MI_CRC32C_OK;
     }
@@ -215,6 +223,7 @@ struct PinBuf
     {
         if (p) (void)hipHostFree(p);
         p = nullptr;
+        dev = nullptr;
         cap = 0;
     }
 };
@@ -497,6 +506,23 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
         if (inits) std::memcpy(hp + count * 12, inits, count * 4);
         if (!src_pinned && hi > lo)
             std::memcpy(hp + data_at, static_cast<const uint8_t*>(base) + lo, hi - lo);
+        // Tiny batches of short records (a single consus::crc32c call): the
+        // direct kernel reads the packed inputs and writes the CRCs in mapped
+        // pinned memory, no copy commands at all (one launch + one sync).
+        if (packed <= kZeroCopyMax && !src_pinned && maxlen_arg <= kDirectMaxRecord &&
+            c->pin_stage.dev && c->pin_out.dev)
+        {
+            const uint8_t* sp = static_cast<const uint8_t*>(c->pin_stage.dev);
+            HIP_TRY(launch_direct(sp + data_at, reinterpret_cast<const uint64_t*>(sp),
+                                  reinterpret_cast<const uint32_t*>(sp + count * 8),
+                                  inits ? reinterpret_cast<const uint32_t*>(sp + count * 12)
+                                        : nullptr,
+                                  count, static_cast<uint32_t*>(c->pin_out.dev), d->d_tables,
+                                  d->d_pow2, d->cus, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            std::memcpy(out, c->pin_out.p, count * 4);
+            return MI_CRC32C_OK;
+        }
         uint8_t* dp = c->off.as<uint8_t>();
         HIP_TRY(hipMemcpyAsync(dp, hp, packed, hipMemcpyHostToDevice, c->stream));
         const uint8_t* dbase = dp + data_at;
