@@ -28,6 +28,12 @@ The JSON line also carries
                 unmodified) on the host cores, over a bounded sample of the
                 same records (rank 0, N=1 only): its dispatched path single-
                 threaded and on up to 16 threads, and its slicing-by-8 path once
+
+Other workloads (--config, one JSON line each; see --help): zipf
+(configs[2]), single (one 4 GiB device record; at N > 1 one record split
+across the GPUs), stream (configs[4], host segments through the H2D/CRC/D2H
+pipeline), pcie4k (configs[1] bytes starting in pinned host memory), dlog
+(durable-log appends/s).
 """
 from __future__ import annotations
 
