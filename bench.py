@@ -64,7 +64,7 @@ KERNEL_MATCH = "crc32c_fixed"             # PMC rows: either fixed-length kernel
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="fixed4k",
                     choices=["fixed4k", "zipf", "stream", "pcie4k", "single", "dlog"],
