@@ -1090,8 +1090,12 @@ __global__ __launch_bounds__(512) void crc32c_finalize_kernel(
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     const uint32_t* __restrict__ partial, const uint32_t* __restrict__ first_pos,
     const uint32_t* __restrict__ int_pos, const uint32_t* __restrict__ last_pos,
-    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables)
+    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
+    const uint32_t* __restrict__ counters, uint64_t item_cap)
 {
+    // a plan larger than the workspace (an understated total_bytes hint) was
+    // not scattered: leave out[] alone rather than read unwritten positions
+    if (counters[kHdrTotal] > item_cap) return;
     __shared__ uint32_t t0[256];
     __shared__ uint32_t zc[1024];
     __shared__ uint32_t zinv[1024];
@@ -1206,7 +1210,8 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
     hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(uint32_t(fin_blocks < 1024 ? fin_blocks : 1024)),
                        dim3(512), 0,
                        stream, b, offsets, lengths, inits, count, ws.partial, ws.first_pos,
-                       ws.int_pos, ws.last_pos, out, tables);
+                       ws.int_pos, ws.last_pos, out, tables,
+                       plan_hdr(ws.blk, var_plan_blocks(count)), ws.item_cap);
     const uint32_t grid = uint32_t(count < 256 ? count : 256);
     hipLaunchKernelGGL(long_finalize_kernel, dim3(grid), dim3(kLongBlock), 0, stream, b, offsets,
                        lengths, inits, plan_hdr(ws.blk, var_plan_blocks(count)), ws.longs, ws.partial,

@@ -106,3 +106,45 @@ def test_device_helper_errors(L, engine):
     _still_works(engine)
     buf.free()
     recv.free()
+
+
+def test_understated_size_hint_leaves_out_unwritten(engine, oracle):
+    """A total_bytes hint below the true sum sizes the plan workspace too
+    small: every plan, chunk and finalize kernel sees the overflow and
+    writes nothing (no out-of-bounds access); the next call with a true
+    hint, or none, is exact."""
+    rng = np.random.default_rng(3)
+    count = 64
+    lengths = np.full(count, 1 << 20, dtype=np.uint32)   # 256+ pieces per record
+    offsets = (np.arange(count, dtype=np.uint64) << np.uint64(20)) + np.uint64(5)
+    size = (count << 20) + 4096
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    data = engine.DeviceBuffer(size)
+    data.upload(buf)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    sentinel = np.full(count, 0xABABABAB, dtype=np.uint32)
+    d_out.upload(sentinel)
+    # in a fresh thread: its own context, so its workspaces are sized by
+    # this call's hint alone (grow-only buffers of earlier calls would fit)
+    import threading
+    errors = []
+
+    def understated():
+        try:
+            engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=4096)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    t = threading.Thread(target=understated)
+    t.start()
+    t.join()
+    assert not errors, errors[0]
+    assert np.array_equal(d_out.download(np.uint32, count), sentinel)
+    want = oracle.batch(buf, offsets, lengths)
+    for hint in (int(lengths.sum()), 0):
+        engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=hint)
+        assert np.array_equal(d_out.download(np.uint32, count), want)
+    for b in (data, d_off, d_len, d_out):
+        b.free()
