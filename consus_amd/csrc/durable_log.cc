@@ -239,15 +239,24 @@ durable_log::durable_log(size_t segment_capacity)
     , m_pinned(true)
     , m_flushes(0)
     , m_frames_flushed(0)
+    , m_stop(false)
+    , m_fsync_delay_us(0)
 {
     for (auto& t : m_flush_ns) t.store(0);
     m_flush = std::thread(&durable_log::flush, this);
+    m_sync = std::thread(&durable_log::sync, this);
 }
 
 durable_log::~durable_log() throw()
 {
     close();
     if (m_flush.joinable()) m_flush.join();
+    {
+        std::lock_guard<std::mutex> hold(m_mtx);
+        m_stop = true;
+        m_cond.notify_all();
+    }
+    if (m_sync.joinable()) m_sync.join();
     for (segment* s : {m_segment_a, m_segment_b})
     {
         if (!s) continue;
@@ -281,6 +290,11 @@ uint64_t durable_log::frames_flushed() const { return m_frames_flushed; }
 void durable_log::flush_seconds(double out[6]) const
 {
     for (int i = 0; i < 6; ++i) out[i] = double(m_flush_ns[i].load()) * 1e-9;
+}
+
+void durable_log::set_fsync_delay_for_testing(uint32_t microseconds)
+{
+    m_fsync_delay_us.store(microseconds);
 }
 
 bool durable_log::open(const std::string& dir)
@@ -509,10 +523,10 @@ int durable_log::error()
     return m_error;
 }
 
-// Checksum the segment's n frames in one batch, patch the CRCs in, write
-// the staged bytes at the end of the file and fsync it.  The frames sit back
-// to back from offset 0, so their offsets come from the length chain.
-int durable_log::flush_segment(segment* seg, uint64_t n, uint64_t used)
+// Checksum the segment's n frames in one batch, patch the CRCs in and write
+// the staged bytes at the end of the file (the sync thread fsyncs it).  The
+// frames sit back to back from offset 0; their offsets come from the slots.
+int durable_log::write_segment(segment* seg, uint64_t n, uint64_t used)
 {
     auto t = std::chrono::steady_clock::now();
     auto lap = [&](int phase) {
@@ -546,10 +560,44 @@ int durable_log::flush_segment(segment* seg, uint64_t n, uint64_t used)
     }
     if (used && !pwrite_all(seg->fd, seg->arena, used, off_t(seg->file_size))) return errno;
     lap(4);
-    if (fsync(seg->fd) < 0) return errno;
-    lap(5);
     seg->file_size += used;
     return 0;
+}
+
+// The sync thread: fsync each written segment in turn and publish its
+// watermark (in write order, so the watermark only grows).  It runs beside
+// the flush thread, which meanwhile checksums and writes the next segment.
+void durable_log::sync()
+{
+    sigset_t ss;
+    if (sigfillset(&ss) == 0) pthread_sigmask(SIG_BLOCK, &ss, nullptr);
+    std::unique_lock<std::mutex> hold(m_mtx);
+    while (true)
+    {
+        m_cond.wait(hold, [&] { return m_stop || !m_pending.empty(); });
+        if (m_pending.empty()) return;  // m_stop
+        const synced job = m_pending.front();
+        hold.unlock();
+        const auto t = std::chrono::steady_clock::now();
+        int e = fsync(job.fd) < 0 ? errno : 0;
+        if (const uint32_t us = m_fsync_delay_us.load()) usleep(us);
+        m_flush_ns[5] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                      std::chrono::steady_clock::now() - t)
+                                      .count());
+        hold.lock();
+        m_pending.erase(m_pending.begin());
+        if (e)
+        {
+            if (m_error == 0) m_error = e;
+        }
+        else if (m_error == 0 || m_error == -1)
+        {
+            m_durable.store(job.upto);
+            ++m_flushes;
+            m_frames_flushed += job.frames;
+        }
+        m_cond.notify_all();
+    }
 }
 
 // Appends move to the other segment (its previous flush is complete: there
@@ -640,17 +688,21 @@ void durable_log::flush()
             std::lock_guard<std::mutex> hold(m_mtx);
             switch_to_next(seg, n);
         }
-        const int e = flush_segment(seg, n, used);
+        const int e = write_segment(seg, n, used);
         {
-            std::lock_guard<std::mutex> hold(m_mtx);
+            std::unique_lock<std::mutex> hold(m_mtx);
             if (e)
-                m_error = e;
-            else
             {
-                m_durable.store(seg->base + n);
-                ++m_flushes;
-                m_frames_flushed += n;
+                m_error = e;
+                m_cond.notify_all();
+                return;
             }
+            // hand the fsync to the sync thread; at most one written segment
+            // waits for it, so appends stay throttled by the disk as with
+            // one segment being fsynced while appends go to the other
+            m_cond.wait(hold, [&] { return m_error != 0 || m_pending.empty(); });
+            if (m_error != 0) return;
+            m_pending.push_back(synced{seg->fd, seg->base + n, n});
             m_cond.notify_all();
         }
     }
@@ -746,6 +798,10 @@ void mi_dlog_flush_seconds(mi_dlog* l, double out[6]) { l->log.flush_seconds(out
 void mi_dlog_set_batch_crc_for_testing(mi_dlog* l, mi_dlog_batch_crc fn, void* ctx)
 {
     l->log.set_batch_crc_for_testing(fn, ctx);
+}
+void mi_dlog_set_fsync_delay_for_testing(mi_dlog* l, uint32_t microseconds)
+{
+    l->log.set_fsync_delay_for_testing(microseconds);
 }
 
 int64_t mi_dlog_scan_file(const char* path, uint64_t* valid_bytes, uint64_t* recnos,

@@ -29,6 +29,8 @@ _SIGS = {
     "mi_dlog_flushes": (C.c_uint64, [C.c_void_p]),
     "mi_dlog_frames_flushed": (C.c_uint64, [C.c_void_p]),
     "mi_dlog_set_batch_crc_for_testing": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mi_dlog_set_fsync_delay_for_testing": (None, [C.c_void_p, C.c_uint32]),
+    "mi_dlog_flush_seconds": (None, [C.c_void_p, C.POINTER(C.c_double)]),
     "mi_dlog_scan_file": (C.c_int64, [C.c_char_p, C.POINTER(C.c_uint64), C.c_void_p, C.c_void_p,
                                       C.c_size_t]),
 }
@@ -93,6 +95,15 @@ class DurableLog:
 
     def frames_flushed(self) -> int:
         return int(_lib().mi_dlog_frames_flushed(self._h))
+
+    def flush_seconds(self) -> list:
+        """copy wait, frame walk, batch CRC, CRC patch, pwrite, fsync (s)."""
+        out = (C.c_double * 6)()
+        _lib().mi_dlog_flush_seconds(self._h, out)
+        return list(out)
+
+    def set_fsync_delay_for_testing(self, microseconds: int) -> None:
+        _lib().mi_dlog_set_fsync_delay_for_testing(self._h, int(microseconds))
 
     def destroy(self) -> None:
         if self._h:

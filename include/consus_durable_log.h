@@ -41,6 +41,8 @@ typedef int (*mi_dlog_batch_crc)(void* ctx, const void* base, const uint64_t* of
                                  const uint32_t* lengths, size_t count, uint64_t total_bytes,
                                  uint32_t* out);
 void mi_dlog_set_batch_crc_for_testing(mi_dlog* log, mi_dlog_batch_crc fn, void* ctx);
+/* Test hook: every fsync also sleeps this long (a slow disk on tmpfs). */
+void mi_dlog_set_fsync_delay_for_testing(mi_dlog* log, uint32_t microseconds);
 
 /* Segment verifier (the reference's missing replay, TODO:2-3): parse the
  * frames of one segment file by their length chain and verify every CRC in

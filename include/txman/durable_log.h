@@ -18,9 +18,11 @@
 // copies the frame into the segment's staging buffer (pinned host memory)
 // and defers its CRC; the flush thread computes the CRCs
 // of every staged frame of the segment in ONE GPU batch
-// (mi_crc32c_batch), patches them in, writes the segment with one pwrite and
-// fsyncs it before publishing the watermark -- so the watermark still covers
-// only records whose CRC bytes are on disk.
+// (mi_crc32c_batch), patches them in and writes the segment with one pwrite;
+// a sync thread fsyncs it and only then publishes the watermark -- so the
+// watermark still covers only records whose CRC bytes are on disk.  The
+// fsync of one segment overlaps the CRC and write of the next (at most one
+// written segment waits for its fsync).
 // replay() -- declared but never defined by the reference (:64, TODO:2-3) --
 // is implemented as a GPU-verified scan of both segment files.
 #ifndef consus_txman_log_h_
@@ -68,16 +70,25 @@ class durable_log
         // Counters for tests and tuning.
         uint64_t flushes() const;
         uint64_t frames_flushed() const;
-        // Seconds spent by the flush thread per phase: copy wait, frame
-        // walk, batch CRC, CRC patch, pwrite, fsync.
+        // Seconds spent per phase: copy wait, frame walk, batch CRC, CRC
+        // patch, pwrite (flush thread), fsync (sync thread).
         void flush_seconds(double out[6]) const;
+        // Test hook: every fsync also sleeps this long (a slow disk on tmpfs).
+        void set_fsync_delay_for_testing(uint32_t microseconds);
 
     private:
         struct segment;
+        struct synced                       // a written segment awaiting fsync
+        {
+            int fd;
+            uint64_t upto;                  // watermark once it is synced
+            uint64_t frames;
+        };
         void flush();
+        void sync();
         int64_t append_slow(segment* seg);
         void switch_to_next(segment* seg, uint64_t n);
-        int flush_segment(segment* seg, uint64_t nframes, uint64_t used);
+        int write_segment(segment* seg, uint64_t nframes, uint64_t used);
 
     private:
         std::string m_path;
@@ -86,6 +97,7 @@ class durable_log
         std::mutex m_mtx;               // flush hand-offs, waiters; never on the append fast path
         std::condition_variable m_cond;
         std::thread m_flush;
+        std::thread m_sync;             // fsyncs written segments, publishes the watermark
         std::atomic<int> m_error;
         bool m_wakeup;
         bool m_opened;
@@ -104,6 +116,9 @@ class durable_log
         std::vector<uint64_t> m_offs;   // flush thread: the sealed segment's frames
         std::vector<uint32_t> m_lens;
         std::vector<uint32_t> m_crcs;
+        std::vector<synced> m_pending;  // under m_mtx: at most one written, unsynced segment
+        bool m_stop;                    // under m_mtx: the destructor ends the sync thread
+        std::atomic<uint32_t> m_fsync_delay_us;
 
     private:
         durable_log(const durable_log&);

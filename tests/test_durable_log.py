@@ -241,3 +241,51 @@ def test_c_abi_refuses_null_arguments(make_log, tmp_path):
     frames = parse_frames(os.path.join(str(tmp_path), "file_a")) + \
         parse_frames(os.path.join(str(tmp_path), "file_b"))
     assert sorted((f[0], f[1]) for f in frames) == [(1, b""), (2, b"after")]
+
+
+def test_slow_fsync_overlaps_next_write(make_log, tmp_path):
+    """A slow disk (every fsync +3 ms): the sync thread fsyncs one written
+    segment while the flush thread checksums and writes the next, at most one
+    segment ahead.  Under 4 appenders and small staging buffers the
+    watermark only grows, never passes an appended record that is not yet
+    on disk, and ends covering every record; replay is intact; fsync time
+    is accounted on the sync thread."""
+    log = make_log(capacity=1 << 14)
+    log.set_fsync_delay_for_testing(3000)
+    assert log.open(str(tmp_path / "d"))
+    got = {}
+    lock = threading.Lock()
+    marks = []
+    stop = threading.Event()
+
+    def watcher():
+        x = log.durable()
+        while not stop.is_set():
+            x = log.wait(x)
+            marks.append(x)
+
+    def worker(t):
+        rng = np.random.default_rng(300 + t)
+        for i in range(250):
+            e = bytes([t]) + rng.integers(0, 256, int(rng.integers(0, 600)), dtype=np.uint8).tobytes()
+            r = log.append(e)
+            assert r > 0
+            with lock:
+                got[r] = e
+    w = threading.Thread(target=watcher)
+    w.start()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    wait_durable(log, 1000)
+    stop.set()
+    log.wake()
+    w.join()
+    assert marks == sorted(marks) and marks[-1] == 1001
+    assert log.frames_flushed() == 1000
+    secs = log.flush_seconds()
+    assert secs[5] >= 0.003 * log.flushes() * 0.9  # the delayed fsyncs, on the sync thread
+    log.close()
+    assert log.replay() == [got[i] for i in range(1, 1001)]

@@ -54,7 +54,9 @@ int main(int argc, char** argv)
 {
     if (argc < 6)
     {
-        fprintf(stderr, "usage: %s DIR THREADS APPENDS_PER_THREAD MIN_ENTRY MAX_ENTRY [SEGMENT_BYTES]\n",
+        fprintf(stderr,
+                "usage: %s DIR THREADS APPENDS_PER_THREAD MIN_ENTRY MAX_ENTRY [SEGMENT_BYTES "
+                "[FSYNC_DELAY_US]]\n",
                 argv[0]);
         return 2;
     }
@@ -63,6 +65,8 @@ int main(int argc, char** argv)
     const uint64_t per = strtoull(argv[3], nullptr, 10);
     const uint32_t lo = uint32_t(atoi(argv[4])), hi = uint32_t(atoi(argv[5]));
     const size_t seg = argc > 6 ? size_t(strtoull(argv[6], nullptr, 10)) : 0;
+    // a slower disk than tmpfs: every fsync also sleeps this long
+    const uint32_t fsync_delay = argc > 7 ? uint32_t(strtoul(argv[7], nullptr, 10)) : 0;
     // diagnosis only: FAKE_CRC=1 replaces the GPU batch with a no-op (CRCs
     // left zero, replay not checked) to time the front-end alone
     const bool fake = getenv("FAKE_CRC") && atoi(getenv("FAKE_CRC"));
@@ -101,6 +105,7 @@ int main(int argc, char** argv)
                 return 0;
             },
             nullptr);
+    log.set_fsync_delay_for_testing(fsync_delay);
     if (!log.open(dir))
     {
         fprintf(stderr, "open(%s) failed: %s\n", dir.c_str(), strerror(log.error()));
