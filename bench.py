@@ -123,7 +123,7 @@ def pmc_traffic(args) -> tuple[float | None, str]:
                        stderr=subprocess.DEVNULL, cwd=out)
     except Exception as e:  # noqa: BLE001 -- traffic is optional, the bench is not
         return None, f"rocprofv3 pass failed: {e}"
-    fixed = args.config in ("fixed4k", "single")  # single: the fixed kernel on its 4 KiB chunks
+    fixed = args.config in ("fixed4k", "single")  # single: the same code on its 4 KiB chunks
     step_kernels = ("plan_", "long_items", "crc32c_chunk_kernel", "crc32c_finalize", "long_finalize")
     vals = []
     for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
@@ -132,7 +132,8 @@ def pmc_traffic(args) -> tuple[float | None, str]:
                 name = row.get("Kernel_Name", "")
                 if row.get("Counter_Name") != "FETCH_SIZE":
                     continue
-                if (fixed and KERNEL_MATCH in name) or \
+                match = "crc32c_span_chunk" if args.config == "single" else KERNEL_MATCH
+                if (fixed and match in name) or \
                         (not fixed and any(k in name for k in step_kernels)):
                     vals.append(float(row["Counter_Value"]))
     shutil.rmtree(out, ignore_errors=True)
@@ -345,14 +346,14 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
             "value": round(n / wall / 2**30, 2), "unit": "GiB/s", "ms_per_step": round(wall * 1e3, 4),
             "data": "synthetic: splitmix64 stream 0xC0DE in HBM (the cfg-2 bytes as one record)",
             "config": {"workload": "1 x 4 GiB record, device-resident, 1 x MI355X; 1,048,575 "
-                                   "aligned 4 KiB chunks through crc32c_fixed_pipe_kernel, "
+                                   "aligned 4 KiB chunks through crc32c_span_chunk_kernel (the fixed kernel's code), "
                                    "head/tail windows and a two-level combine tree on the GPU"},
             "roofline": {"bound": "hbm", "achieved": round(n / wall / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(n / wall / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic[0] is None else round(traffic[0]),
-                         "traffic_note": traffic[1] + " (crc32c_fixed_pipe_kernel, per call)",
-                         "kernel": "crc32c_fixed_pipe_kernel + single_tree + single_join "
+                         "traffic_note": traffic[1] + " (crc32c_span_chunk_kernel, per call)",
+                         "kernel": "crc32c_span_chunk_kernel + single_tree + single_join "
                                    "(whole call, host sync included)"},
             "digest_verified": ok, "crc": f"{got:#010x}"})
         return res
@@ -482,7 +483,7 @@ def run_single_split(args, E, dist, rank, world):
             "roofline": {"bound": "hbm", "achieved": round(n / per / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(n / per / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "per-rank slice: crc32c_fixed_pipe_kernel + single_tree + "
+                         "kernel": "per-rank slice: crc32c_span_chunk_kernel + single_tree + "
                                    "single_join (host sync included)"},
             "exchange_ms": round(exch * 1e3, 3),
             "digest_verified": (whole == want) if want is not None else None,

@@ -283,10 +283,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_kernel(
 // loop-carried buffer is the same 8 loads on every path into the header and
 // the compiler's vmcnt accounting stays exact.
 template <int G, bool INITS>
-__global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_pipe_kernel(
-    const uint8_t* __restrict__ base, uint64_t stride, const uint32_t* __restrict__ inits,
-    uint64_t init_stride, uint64_t count, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables)
+__device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uint64_t stride,
+                                           const uint32_t* __restrict__ inits,
+                                           uint64_t init_stride, uint64_t count,
+                                           uint32_t* __restrict__ out,
+                                           const uint32_t* __restrict__ tables)
 {
     static_assert(G % 2 == 0, "buffers alternate per group");
     stage_tables(tables);
@@ -343,6 +344,24 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_pipe_kernel(
         rec = next;
         if (INITS) init_word = next_init;
     }
+}
+
+template <int G, bool INITS>
+__global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_pipe_kernel(
+    const uint8_t* __restrict__ base, uint64_t stride, const uint32_t* __restrict__ inits,
+    uint64_t init_stride, uint64_t count, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables)
+{
+    fixed_pipe<G, INITS>(base, stride, inits, init_stride, count, out, tables);
+}
+
+// The same code over launch_single's 4 KiB chunks of one record, under a
+// name of its own so that a profile tells it apart from record batches.
+__global__ __launch_bounds__(kBlock, 1) void crc32c_span_chunk_kernel(
+    const uint8_t* __restrict__ base, uint64_t count, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables)
+{
+    fixed_pipe<4, false>(base, kChunk, tables + kTabZero, 0, count, out, tables);
 }
 
 hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const uint32_t* inits,
@@ -1429,7 +1448,7 @@ hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const ui
 // One large device buffer (consus::crc32c(init, data, n), common/crc32c.cc:
 // 122-126, on a device pointer).  The buffer [a, a + n) is cut as
 //   head      [a, E)            4 <= h = E - a < 4100 bytes, E 4 KiB-aligned
-//   interior  m chunks of 4 KiB from E (crc32c_fixed_pipe_kernel, init 0)
+//   interior  m chunks of 4 KiB from E (crc32c_span_chunk_kernel, init 0)
 //   tail      t < 4096 bytes
 // and joined with raw-register algebra:
 //   raw(chunk j) = crc_j ^ crc0,  crc0 = crc32c(0, 4096 zero bytes)
@@ -1590,8 +1609,10 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
     if (m == 0 || nblocks > 1024 || 22 + log_r + 9 >= kSingleStaged || (m >> 24) != 0)
         return hipErrorInvalidValue;
     const uint8_t* base = static_cast<const uint8_t*>(data) + h;
-    const hipError_t e = launch_fixed(base, kChunk, kChunk, nullptr, m, crcs, tables, grid, stream);
-    if (e != hipSuccess) return e;
+    const uint64_t need = (m + (kBlock / kTeam) - 1) / (kBlock / kTeam);
+    if (uint64_t(grid) > need) grid = int(need);
+    hipLaunchKernelGGL(crc32c_span_chunk_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream, base,
+                       m, crcs, tables);
     hipLaunchKernelGGL(single_tree_kernel, dim3(nblocks + 2), dim3(1024), 0, stream, crcs, M - m,
                        crc0, log_r, uint64_t(data), h, m, t, init, tables, pow2, vals);
     hipLaunchKernelGGL(single_join_kernel, dim3(1), dim3(1024), kSingleStaged * 4096, stream, m,
@@ -1603,6 +1624,7 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
 hipError_t configure_kernels()
 {
     const void* k[] = {reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<4, false>),
+                       reinterpret_cast<const void*>(&crc32c_span_chunk_kernel),
                        reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<4, true>),
                        reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<2, false>),
                        reinterpret_cast<const void*>(&crc32c_fixed_pipe_kernel<2, true>),
