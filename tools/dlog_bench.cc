@@ -16,6 +16,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <string>
@@ -119,6 +120,11 @@ int main(int argc, char** argv)
     std::atomic<bool> go{false};
     std::atomic<uint64_t> failures{0};
     std::vector<std::thread> ths;
+    // durability latency: every 64th append's return time against the first
+    // watermark the monitor sees that covers it (commit latency of txman)
+    std::vector<std::vector<std::pair<int64_t, double>>> samples(threads);
+    std::vector<std::pair<double, int64_t>> marks;
+    std::atomic<bool> stop{false};
     for (int t = 0; t < threads; ++t)
         ths.emplace_back([&, t] {
             ready.fetch_add(1);
@@ -131,10 +137,20 @@ int main(int argc, char** argv)
                     failures.fetch_add(1);
                     continue;
                 }
+                if ((k & 63) == 0) samples[t].emplace_back(r, now());
                 rec_len[r - 1] = lens[t][k];
                 rec_at[r - 1] = offs[t][k];
             }
         });
+    std::thread monitor([&] {
+        int64_t w = log.durable();
+        while (!stop.load())
+        {
+            w = log.wait(w);
+            marks.emplace_back(now(), w);
+            if (log.error()) break;
+        }
+    });
     while (ready.load() < threads) std::this_thread::yield();
     const double t0 = now();
     go.store(true, std::memory_order_release);
@@ -143,6 +159,22 @@ int main(int argc, char** argv)
     int64_t x = log.durable();
     while (x <= int64_t(total) && !log.error()) x = log.wait(x);
     const double t_durable = now();
+    stop.store(true);
+    log.wake();
+    monitor.join();
+    std::vector<double> lat;
+    for (const auto& v : samples)
+        for (const auto& [r, ta] : v)
+        {
+            // first mark whose watermark exceeds r (marks are in watermark order)
+            auto it = std::upper_bound(marks.begin(), marks.end(), r,
+                                       [](int64_t rr, const std::pair<double, int64_t>& m) {
+                                           return rr < m.second;
+                                       });
+            if (it != marks.end()) lat.push_back(std::max(0.0, it->first - ta) * 1e6);
+        }
+    std::sort(lat.begin(), lat.end());
+    auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[size_t(q * (lat.size() - 1))]; };
     const uint64_t flushes = log.flushes(), frames = log.frames_flushed();
     const int err = log.error();
     double fs[6];
@@ -166,12 +198,15 @@ int main(int argc, char** argv)
            "\"frame_GiB_per_s\": %.4f, \"flushes\": %llu, \"frames_flushed\": %llu, "
            "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
            "\"flush_s\": {\"copy_wait\": %.4f, \"walk\": %.4f, \"batch_crc\": %.4f, "
-           "\"patch\": %.4f, \"pwrite\": %.4f, \"fsync\": %.4f}}\n",
+           "\"patch\": %.4f, \"pwrite\": %.4f, \"fsync\": %.4f}, "
+           "\"durable_latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, "
+           "\"samples\": %zu}}\n",
            threads, (unsigned long long)total, (unsigned long long)entry_bytes,
            (unsigned long long)frame_bytes, t_appended - t0, t_durable - t0,
            double(total) / (t_durable - t0), double(frame_bytes) / (t_durable - t0) / (1u << 30),
            (unsigned long long)flushes, (unsigned long long)frames,
            (unsigned long long)failures.load(), err, (long long)n, (unsigned long long)rp.bad,
-           fs[0], fs[1], fs[2], fs[3], fs[4], fs[5]);
+           fs[0], fs[1], fs[2], fs[3], fs[4], fs[5], pct(0.5), pct(0.99),
+           lat.empty() ? 0.0 : lat.back(), lat.size());
     return (failures.load() || err || n != int64_t(total) || rp.bad) ? 1 : 0;
 }
