@@ -491,6 +491,95 @@ def run_single_split(args, E, dist, rank, world):
     dist.destroy_process_group()
 
 
+def run_zipf_sharded(args, E, dist, rank, world):
+    """configs[2]'s record stream continued to world x R records (R = 1M per
+    rank), split into contiguous record ranges balanced by BYTES
+    (shard.balanced_ranges); rank r generates exactly its
+    records' bytes in its HBM and runs the device-resident variable path on
+    them.  Timed: the steps between barriers, max over ranks.  Verified: the
+    ranks' CRC-vector digests, combined with their record counts, against
+    the golden digest of the whole stream prefix (combine of 1M-record block
+    digests)."""
+    import torch
+    from consus_amd import shard
+    from consus_amd import workload as W
+    R = args.records_per_rank
+    n = world * R
+    lengths = E.zipf_lengths(W.ZIPF_SEED, n)
+    offsets = np.zeros(n, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    lo, hi = shard.balanced_ranges(lengths, world)[rank]
+    cnt = hi - lo
+    start = int(offsets[lo]) if cnt else 0
+    a = start & ~7                                  # the fill wants 8-byte aligned offsets
+    nbytes = (int(offsets[hi - 1]) + int(lengths[hi - 1]) - a) if cnt else 0
+    local_total = int(lengths[lo:hi].sum(dtype=np.uint64))
+    data = E.DeviceBuffer(nbytes + 16)
+    if nbytes:
+        data.fill_splitmix64(W.DATA_SEED, byte_offset=a, nbytes=(nbytes + 7) & ~7)
+    d_off, d_len, out = (E.DeviceBuffer(max(cnt, 1) * 8), E.DeviceBuffer(max(cnt, 1) * 4),
+                         E.DeviceBuffer(max(cnt, 1) * 4))
+    if cnt:
+        d_off.upload(offsets[lo:hi] - np.uint64(a))
+        d_len.upload(lengths[lo:hi])
+
+    def step(asynchronous):
+        if cnt:
+            E.device_batch(data, d_off, d_len, cnt, out, total_bytes=local_total,
+                           asynchronous=asynchronous)
+    for _ in range(args.warmup):
+        step(False)
+    E.sync()
+    dist.barrier()
+    E.sync()
+    t0 = time.perf_counter()
+    E.timer_start()
+    for _ in range(args.steps):
+        step(True)
+    ev = E.timer_stop()
+    E.sync()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall, ev], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, ev_max = float(t[0]), float(t[1])
+    dig = E.crc32c_device(out, cnt * 4) if cnt else 0
+    got = [None] * world
+    dist.all_gather_object(got, (dig, cnt, local_total, ev))
+    if rank == 0:
+        blocks = golden_digests().get("zipf_seed0x5eed_data0xda7a5eed_blocks", {})
+        bd = blocks.get("block_digests", [])
+        ok = None
+        if R == 1 << 20 and len(bd) >= world:
+            want = shard.combine_digests(bd[:world], [1 << 20] * world)
+            ok = shard.combine_digests([g[0] for g in got], [g[1] for g in got]) == want
+        total = sum(g[2] for g in got)
+        per = wall / args.steps
+        # per-GPU rate of the slowest rank: its bytes over its own step time
+        achieved = min(g[2] / (g[3] / args.steps * 1e-3) / 1e9 for g in got if g[1])
+        print(json.dumps({
+            "metric": "GiB/s CRC32C over device-resident mixed-length records (Zipf 64 B-64 KiB)",
+            "value": round(total / per / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: config-3 Zipf lengths continued to N x 1M records, splitmix64 "
+                    "stream 0xDA7A5EED, each rank's bytes generated in its HBM",
+            "config": {"workload": f"{n} mixed-length records sharded by bytes over {world} x "
+                                   "MI355X (configs[2] per GPU)",
+                       "total_bytes": total, "records_per_rank": [g[1] for g in got],
+                       "bytes_per_rank": [g[2] for g in got],
+                       "parallelism": f"byte-balanced record shards x{world}, no collective in "
+                                      "the timed region"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None,
+                         "kernel": "plan + crc32c_chunk_kernel + finalize (whole step; the "
+                                   "slowest rank's bytes over its own step time)"},
+            "digest_verified": ok, "digests": [f"{g[0]:#010x}" for g in got],
+            "cpu_baseline": None}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -516,9 +605,9 @@ def main():
     # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.
     import consus_amd as E
     E.init(0 if args.share_device else local)
-    if args.config != "fixed4k" and not (args.config == "single" and world > 1):
+    if args.config != "fixed4k" and not (args.config in ("single", "zipf") and world > 1):
         if world != 1:
-            sys.exit("secondary configs other than single run on one GPU")
+            sys.exit("secondary configs other than single and zipf run on one GPU")
         res = run_secondary(args, E, (traffic, traffic_note))
         if not args.child_pmc:
             print(json.dumps(res), flush=True)
@@ -541,6 +630,9 @@ def main():
 
     if args.config == "single":  # world > 1: one record split across the ranks
         run_single_split(args, E, dist, rank, world)
+        return
+    if args.config == "zipf":  # world > 1: the record stream sharded by bytes
+        run_zipf_sharded(args, E, dist, rank, world)
         return
 
     R, L = args.records_per_rank, args.record_bytes

@@ -173,6 +173,26 @@ def main() -> None:
         "total_bytes": int(lz.sum(dtype=np.uint64)), "length_digest": orc.digest(lz)[0],
         "digest": dz, "xor": xz, "first16": [int(v) for v in cz[:16]],
     }
+    # the same Zipf record stream continued to 8M records, as 8 blocks of 1M
+    # (bench.py --config zipf at N > 1 shards it by bytes across the ranks)
+    nz = 8 * block
+    lz8 = consus_amd.zipf_lengths(0x5EED, nz)
+    assert np.array_equal(lz8[:block], lz)
+    oz8 = np.zeros(nz, dtype=np.uint64)
+    oz8[1:] = np.cumsum(lz8[:-1], dtype=np.uint64)
+    zblocks = []
+    for k in range(8):
+        ck = cz if k == 0 else ref.splitmix_var(0xDA7A5EED, oz8[k * block:(k + 1) * block],
+                                                 lz8[k * block:(k + 1) * block], threads=THREADS)
+        zblocks.append(orc.digest(ck)[0])
+    assert zblocks[0] == dz
+    digests["zipf_seed0x5eed_data0xda7a5eed_blocks"] = {
+        "definition": "records [k 2^20, (k+1) 2^20) of the config-3 stream (lengths "
+                      "mi_workload_zipf_lengths(0x5EED, 0, 8 x 2^20), packed back to back from offset "
+                      "0 of the splitmix64 stream 0xDA7A5EED); digest = crc32c(0, LE CRC vector)",
+        "block_digests": zblocks,
+        "total_bytes_8M": int(lz8.sum(dtype=np.uint64)),
+    }
     # cfg 5: 64 MiB durable-log segments (consus_amd/workload.py recipe)
     from consus_amd.workload import log_segments
     segs = []

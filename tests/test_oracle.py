@@ -119,3 +119,12 @@ def test_random_vs_reference(oracle, reference):
         assert oracle.crc32c(init, buf, n, off) == exp
         assert oracle.crc32c(init, buf, n, off, impl="sb8") == exp
         assert reference.crc32c(init, buf, n, off, impl="sw") == exp
+
+
+def test_zipf_block_goldens_extend_the_1M_golden():
+    """The 8 x 1M-record Zipf block digests (bench.py --config zipf at N > 1)
+    start with the configs[2] golden itself."""
+    d = load("digests.json")
+    blocks = d["zipf_seed0x5eed_data0xda7a5eed_blocks"]["block_digests"]
+    assert len(blocks) == 8
+    assert blocks[0] == d["zipf_seed0x5eed_data0xda7a5eed_1048576"]["digest"]

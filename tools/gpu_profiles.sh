@@ -38,4 +38,6 @@ run bench_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-pe
     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --share-device --steps 5 --warmup 2 --no-cpu
 run bench_single_split_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --config single --share-device --steps 10 --warmup 2
+run bench_zipf_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --config zipf --share-device --steps 10 --warmup 2
 echo "ALL OK"
