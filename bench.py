@@ -30,7 +30,7 @@ The JSON line also carries
                 threaded and on up to 16 threads, and its slicing-by-8 path once
 
 Other workloads (--config, one JSON line each; see --help): zipf
-(configs[2]), single (one 4 GiB device record; at N > 1 one record split
+(configs[2]; at N > 1 sharded by bytes across the GPUs), single (one 4 GiB device record; at N > 1 one record split
 across the GPUs), stream (configs[4], host segments through the H2D/CRC/D2H
 pipeline), pcie4k (configs[1] bytes starting in pinned host memory), dlog
 (durable-log appends/s).
@@ -68,7 +68,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="fixed4k",
                     choices=["fixed4k", "zipf", "stream", "pcie4k", "single", "dlog"],
-                    help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2]; "
+                    help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2] "
+                         "(at N > 1 its stream continued to N x 1M records, sharded by bytes); "
                          "stream = configs[4] (64 MiB host segments, H2D+CRC+D2H); pcie4k = "
                          "configs[1] bytes starting in pinned host memory; single = the same "
                          "4 GiB as ONE device-resident record (long-record path, SURVEY 8(f)4; "
