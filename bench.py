@@ -157,8 +157,9 @@ def rccl_gather(E, dist, rank: int, world: int, out, R: int, digests, rec) -> di
     """All-gather every rank's CRC vector over RCCL (xGMI), outside the timed
     region; rank 0 checks each gathered block against the rank's own digest.
     A watchdog ends every rank if RCCL never returns; rank 0 first prints its
-    bench line (`rec`) with the gather marked as timed out.  Every rank then
-    exits 0: the gather is optional evidence, the timed bench line is not."""
+    bench line (`rec`) with the gather marked as timed out, then every rank
+    exits 3, so the launcher sees the hung collective (the bench line above
+    it stays valid: the gather is outside the timed region)."""
     import threading
     done = threading.Event()
 
@@ -168,7 +169,7 @@ def rccl_gather(E, dist, rank: int, world: int, out, R: int, digests, rec) -> di
                 rec["gather"] = {"collective": "rccl all-gather", "error": "timed out after 120 s"}
                 print(json.dumps(rec), flush=True)
             print(f"rank {rank}: RCCL gather timed out after 120 s", file=sys.stderr, flush=True)
-            os._exit(0)
+            os._exit(3)
     threading.Thread(target=watchdog, daemon=True).start()
     try:
         uid = [E.comm_unique_id() if rank == 0 else None]

@@ -3,8 +3,11 @@
 Python mirror of the reference operator interface (``consus::crc32c``,
 common/crc32c.h:40-41) over the C ABI of ``include/consus_crc32c.h``
 (``consus_amd/lib/libconsus_crc32c.so``).  Every checksum is computed by the
-HIP kernels; if the library or a gfx950 device is missing, calls raise
-``EngineError`` -- there is no CPU fallback.
+HIP kernels; if the library is missing, or a gfx950 device is missing, these
+calls raise ``EngineError``.  (Only the C drop-in ``mi_crc32c`` /
+``consus::crc32c`` and calls made with FLAG_FALLBACK complete on the
+engine's CPU path after an engine failure, and every such completion is
+counted: ``stats()``.)
 
     from consus_amd import crc32c, crc32c_batch
     crc32c(0, b"123456789")            # -> 0xE3069283, same as consus::crc32c
@@ -32,6 +35,8 @@ ERCCL = -71
 FLAG_DEVICE = 0x1
 FLAG_ASYNC = 0x2
 FLAG_PLANNED = 0x4  # force plan -> chunks -> finalize (no one-launch direct kernel)
+FLAG_FALLBACK = 0x8  # host memory: complete on the engine's CPU path if the GPU fails (counted)
+ERANGE = -34
 MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D = 1, 2, 3
 
 
@@ -86,7 +91,26 @@ _SIGS = {
     "mi_comm_allgather_u32": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
     "mi_comm_destroy": (C.c_int, []),
     "mi_workload_zipf_lengths": (None, [C.c_uint64, C.c_uint64, C.c_size_t, C.c_void_p]),
+    "mi_crc32c_device_count": (C.c_int, []),
+    "mi_crc32c_stats": (None, [C.c_void_p]),
+    "mi_crc32c_stats_reset": (None, []),
+    "mi_crc32c_batch_multi": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_size_t, C.c_uint64, C.c_void_p, C.c_uint,
+                                        C.c_void_p, C.c_int, C.c_uint64]),
+    "mi_crc32c_batch_fixed_multi": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                              C.c_size_t, C.c_void_p, C.c_uint, C.c_void_p,
+                                              C.c_int, C.c_uint64]),
+    "mi_crc32c_balanced_ranges": (None, [C.c_void_p, C.c_size_t, C.c_int, C.c_uint64,
+                                         C.c_void_p]),
 }
+
+
+class Stats(C.Structure):
+    """mi_crc32c_stats_t (include/consus_crc32c.h)."""
+    _fields_ = [("gpu_calls", C.c_uint64), ("fallback_calls", C.c_uint64),
+                ("fallback_bytes", C.c_uint64), ("sharded_calls", C.c_uint64),
+                ("last_fallback_status", C.c_int32),
+                ("reserved", C.c_int32)]
 
 _lib = None
 
@@ -156,7 +180,15 @@ def zipf_lengths(seed: int, count: int, first: int = 0) -> np.ndarray:
     return out
 
 
-def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False) -> np.ndarray:
+def crc32c_dropin(init_crc: int, data) -> int:
+    """The C drop-in mi_crc32c (= consus::crc32c): total, never raises; an
+    engine failure completes on the CPU path and shows in stats()."""
+    a = _as_u8(data)
+    return int(lib().mi_crc32c(init_crc & 0xFFFFFFFF, C.c_void_p(a.ctypes.data), a.size))
+
+
+def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False,
+                 fallback: bool = False) -> np.ndarray:
     """Per-record CRCs of host records [buf + off, +len)."""
     a = _as_u8(buf)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -169,18 +201,90 @@ def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False) -> np
     out = np.zeros(off.size, dtype=np.uint32)
     _check(lib().mi_crc32c_batch(C.c_void_p(a.ctypes.data), _np_ptr(off), _np_ptr(ln),
                                  _np_ptr(ini), off.size, int(ln.sum(dtype=np.uint64)),
-                                 _np_ptr(out), FLAG_PLANNED if planned else 0), "mi_crc32c_batch")
+                                 _np_ptr(out), (FLAG_PLANNED if planned else 0) |
+                                 (FLAG_FALLBACK if fallback else 0)), "mi_crc32c_batch")
     return out
 
 
-def crc32c_fixed(buf, stride: int, length: int, count: int, inits=None) -> np.ndarray:
+def crc32c_fixed(buf, stride: int, length: int, count: int, inits=None,
+                 fallback: bool = False) -> np.ndarray:
     a = _as_u8(buf)
     if count and (count - 1) * stride + length > a.size:
         raise ValueError("records outside buffer")
     ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
     out = np.zeros(count, dtype=np.uint32)
     _check(lib().mi_crc32c_batch_fixed(C.c_void_p(a.ctypes.data), stride, length, _np_ptr(ini),
-                                       count, _np_ptr(out), 0), "mi_crc32c_batch_fixed")
+                                       count, _np_ptr(out), FLAG_FALLBACK if fallback else 0),
+           "mi_crc32c_batch_fixed")
+    return out
+
+
+def stats() -> dict:
+    """Process-wide counters: GPU-completed calls and CPU-path fallbacks."""
+    s = Stats()
+    lib().mi_crc32c_stats(C.byref(s))
+    return {f: int(getattr(s, f)) for f, _ in Stats._fields_ if f != "reserved"}
+
+
+def stats_reset() -> None:
+    lib().mi_crc32c_stats_reset()
+
+
+def device_count() -> int:
+    """Usable gfx950 devices (not initialised)."""
+    return int(lib().mi_crc32c_device_count())
+
+
+def balanced_ranges(lengths, k: int) -> list[tuple[int, int]]:
+    """The engine's byte-balanced split rule (mi_crc32c_balanced_ranges)."""
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    bounds = np.zeros(k + 1, dtype=np.uint64)
+    lib().mi_crc32c_balanced_ranges(_np_ptr(ln), ln.size, k, int(ln.sum(dtype=np.uint64)),
+                                    _np_ptr(bounds))
+    return [(int(bounds[r]), int(bounds[r + 1])) for r in range(k)]
+
+
+def _dev_list(devices):
+    if devices is None:
+        return None, 0
+    d = (C.c_int * len(devices))(*devices)
+    return d, len(devices)
+
+
+def crc32c_batch_multi(buf, offsets, lengths, inits=None, devices=None, shard_min: int = 0,
+                       fallback: bool = False, planned: bool = False) -> np.ndarray:
+    """Per-record CRCs of a host batch sharded by bytes over several devices
+    (mi_crc32c_batch_multi).  devices=None: every usable device."""
+    a = _as_u8(buf)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if off.size != ln.size:
+        raise ValueError("offsets/lengths size mismatch")
+    if off.size and int((off + ln.astype(np.uint64)).max()) > a.size:
+        raise ValueError("record outside buffer")
+    ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+    out = np.zeros(off.size, dtype=np.uint32)
+    dl, nd = _dev_list(devices)
+    flags = (FLAG_FALLBACK if fallback else 0) | (FLAG_PLANNED if planned else 0)
+    _check(lib().mi_crc32c_batch_multi(C.c_void_p(a.ctypes.data), _np_ptr(off), _np_ptr(ln),
+                                       _np_ptr(ini), off.size, int(ln.sum(dtype=np.uint64)),
+                                       _np_ptr(out), flags, dl, nd, shard_min),
+           "mi_crc32c_batch_multi")
+    return out
+
+
+def crc32c_fixed_multi(buf, stride: int, length: int, count: int, inits=None, devices=None,
+                       shard_min: int = 0, fallback: bool = False) -> np.ndarray:
+    a = _as_u8(buf)
+    if count and (count - 1) * stride + length > a.size:
+        raise ValueError("records outside buffer")
+    ini = None if inits is None else np.ascontiguousarray(inits, dtype=np.uint32)
+    out = np.zeros(count, dtype=np.uint32)
+    dl, nd = _dev_list(devices)
+    _check(lib().mi_crc32c_batch_fixed_multi(C.c_void_p(a.ctypes.data), stride, length,
+                                             _np_ptr(ini), count, _np_ptr(out),
+                                             FLAG_FALLBACK if fallback else 0, dl, nd, shard_min),
+           "mi_crc32c_batch_fixed_multi")
     return out
 
 
@@ -294,7 +398,12 @@ class PinnedBuffer:
 
 class Pipeline:
     """H2D -> CRC -> D2H of host segments overlapped over `depth` HIP streams
-    (mi_crc32c_pipeline_*).  Results land in `out` at wait(ticket)."""
+    (mi_crc32c_pipeline_*).  Results land in `out` at wait(ticket).
+
+    A pageable segment (bytes, numpy array) is copied into pinned staging by
+    submit() and may be reused at once.  A PinnedBuffer segment is DMA'd in
+    place: do not modify it until wait(ticket) returns (include/consus_crc32c.h).
+    """
 
     def __init__(self, max_segment_bytes: int, max_records: int, depth: int = 2):
         h = C.c_void_p(0)

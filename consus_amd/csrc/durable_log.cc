@@ -25,11 +25,12 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <new>
 #include <chrono>
+#include <new>
 
 #include "../../include/consus_crc32c.h"
 #include "../../include/consus_durable_log.h"
+#include "host_crc.h"
 
 using consus::durable_log;
 
@@ -63,11 +64,25 @@ uint32_t unpack32be(const unsigned char* p)
     return v;
 }
 
-int gpu_batch(void*, const void* base, const uint64_t* off, const uint32_t* len, size_t n,
+// The default batch engine: the GPU, sharded over the configured devices for
+// large segments (mi_crc32c_batch_multi applies the amortisation threshold),
+// completed on the engine's CPU path if the GPU fails (MI_CRC32C_FALLBACK:
+// the log never turns an engine failure into EIO; the fallback is counted in
+// mi_crc32c_stats).
+int gpu_batch(void* ctx, const void* base, const uint64_t* off, const uint32_t* len, size_t n,
               uint64_t total, uint32_t* out)
 {
-    return mi_crc32c_batch(base, off, len, nullptr, n, total, out, 0);
+    const auto* o = static_cast<const consus::durable_log_options*>(ctx);
+    const int gpus = o ? o->gpus : 0;
+    if (gpus == 1)
+        return mi_crc32c_batch(base, off, len, nullptr, n, total, out, MI_CRC32C_FALLBACK);
+    return mi_crc32c_batch_multi(base, off, len, nullptr, n, total, out, MI_CRC32C_FALLBACK,
+                                 nullptr, gpus, o ? o->shard_min_bytes : 0);
 }
+
+// Frames longer than this are checksummed one by one (single-buffer path)
+// rather than inside a batch, whose lengths are 32-bit.
+constexpr uint64_t kBatchFrameMax = uint64_t(1) << 30;
 
 bool pwrite_all(int fd, const unsigned char* p, size_t n, off_t off)
 {
@@ -90,44 +105,93 @@ struct Frame
 {
     uint64_t recno;
     uint64_t offset;  // of the frame in the file / buffer
-    uint32_t length;  // of the entry
+    uint64_t length;  // of the entry
 };
 
-// Parse frames by their length chain and verify every CRC in one batch.
-// Returns the number of leading complete, CRC-valid frames, or -1 if the
-// engine failed.  A torn tail or the first bad CRC ends the scan.
+// Parse frames by their length chain and verify every CRC: frames up to
+// kBatchFrameMax in one batch, longer ones one by one (`single`).  Returns the
+// number of leading complete, CRC-valid frames, or -1 if the engine failed.
+// A torn tail or the first bad CRC ends the scan.
+template <typename Single>
 int64_t scan_frames(const unsigned char* buf, uint64_t size, consus::durable_log_batch_crc fn,
-                    void* ctx, std::vector<Frame>* frames, uint64_t* valid_bytes)
+                    void* ctx, Single single, std::vector<Frame>* frames, uint64_t* valid_bytes)
 {
-    std::vector<uint64_t> offs;
-    std::vector<uint32_t> lens, stored;
-    std::vector<uint64_t> recnos;
-    uint64_t pos = 0, total = 0;
+    std::vector<uint64_t> offs, recnos, lens;
+    std::vector<uint32_t> stored;
+    uint64_t pos = 0;
     while (size - pos >= kHeader + kTrailer)
     {
         const uint64_t recno = unpack64be(buf + pos);
         const uint64_t len = unpack64be(buf + pos + 8);
-        if (len > size - pos - kHeader - kTrailer || len > UINT32_MAX - kHeader) break;  // torn
+        if (len > size - pos - kHeader - kTrailer) break;  // torn
         offs.push_back(pos);
-        lens.push_back(uint32_t(kHeader + len));
+        lens.push_back(kHeader + len);
         stored.push_back(unpack32be(buf + pos + kHeader + len));
         recnos.push_back(recno);
-        total += kHeader + len;
         pos += kHeader + len + kTrailer;
     }
     std::vector<uint32_t> crcs(offs.size());
-    if (!offs.empty() && fn(ctx, buf, offs.data(), lens.data(), offs.size(), total, crcs.data()) != 0)
+    std::vector<uint64_t> boffs;
+    std::vector<uint32_t> blens;
+    std::vector<size_t> which;
+    uint64_t total = 0;
+    for (size_t i = 0; i < offs.size(); ++i)
+    {
+        if (lens[i] > kBatchFrameMax)
+        {
+            crcs[i] = single(buf + offs[i], lens[i]);
+            continue;
+        }
+        boffs.push_back(offs[i]);
+        blens.push_back(uint32_t(lens[i]));
+        which.push_back(i);
+        total += lens[i];
+    }
+    std::vector<uint32_t> bcrcs(boffs.size());
+    if (!boffs.empty() &&
+        fn(ctx, buf, boffs.data(), blens.data(), boffs.size(), total, bcrcs.data()) != 0)
         return -1;
+    for (size_t j = 0; j < which.size(); ++j) crcs[which[j]] = bcrcs[j];
     size_t good = 0;
     uint64_t bytes = 0;
     while (good < offs.size() && crcs[good] == stored[good])
     {
-        if (frames) frames->push_back(Frame{recnos[good], offs[good], lens[good] - uint32_t(kHeader)});
+        if (frames) frames->push_back(Frame{recnos[good], offs[good], lens[good] - kHeader});
         bytes += lens[good] + kTrailer;
         ++good;
     }
     if (valid_bytes) *valid_bytes = bytes;
     return int64_t(good);
+}
+
+// A batch engine whose failures the engine's CPU path completes (counted).
+struct Chained
+{
+    consus::durable_log_batch_crc fn;
+    void* ctx;
+};
+
+int batch_or_host(void* c, const void* base, const uint64_t* off, const uint32_t* len, size_t n,
+                  uint64_t total, uint32_t* out)
+{
+    const auto* ch = static_cast<const Chained*>(c);
+    if (ch->fn(ch->ctx, base, off, len, n, total, out) == 0) return 0;
+    mi_host::batch(base, off, len, nullptr, n, out);
+    mi_host::note_fallback(MI_CRC32C_EHIP, total);
+    return 0;
+}
+
+// One frame's CRC on the engine's single-buffer path (completes on the CPU
+// path if the GPU fails).
+uint32_t single_crc(const unsigned char* p, uint64_t n)
+{
+    uint32_t c = 0;
+    if (mi_crc32c_buffer(0, p, size_t(n), &c, MI_CRC32C_FALLBACK) != MI_CRC32C_OK)
+    {
+        c = mi_host::crc32c(0, p, size_t(n));
+        mi_host::note_fallback(MI_CRC32C_EINVAL, n);
+    }
+    return c;
 }
 
 bool read_file(int dirfd, const char* name, std::vector<unsigned char>* out)
@@ -168,6 +232,8 @@ constexpr int kIdxShift = 40;
 constexpr uint64_t kUsedMask = (uint64_t(1) << kIdxShift) - 1;
 constexpr uint64_t kMaxFrames = (uint64_t(1) << (63 - kIdxShift)) - 1;
 constexpr unsigned kDoneShards = 16;
+// at_slot(i) of a frame staged outside the arena (see segment::ext)
+constexpr uint64_t kExternal = uint64_t(1) << 63;
 
 struct durable_log::segment
 {
@@ -207,6 +273,19 @@ struct durable_log::segment
     {
         for (Shard& d : done) d.n.store(0);
     }
+    // Frames too large for the staging arena (more than half of it) take a
+    // slot and a record number like any other (0 arena bytes reserved) but
+    // are staged in a buffer of their own, listed here until the flush
+    // writes them in record order between the arena's frames.
+    struct External
+    {
+        uint64_t idx;
+        unsigned char* frame;  // header, entry, room for the CRC
+        uint64_t bytes;
+    };
+    std::mutex ext_mu;
+    std::vector<External> ext;
+    bool pinned = false;  // arena from mi_host_malloc_pinned (else malloc)
 };
 
 static unsigned done_shard()
@@ -216,9 +295,20 @@ static unsigned done_shard()
     return k;
 }
 
-durable_log::durable_log() : durable_log(kDefaultCapacity) {}
+namespace {
+consus::durable_log_options with_capacity(size_t cap)
+{
+    consus::durable_log_options o;
+    o.segment_capacity = cap;
+    return o;
+}
+}  // namespace
 
-durable_log::durable_log(size_t segment_capacity)
+durable_log::durable_log() : durable_log(durable_log_options()) {}
+
+durable_log::durable_log(size_t segment_capacity) : durable_log(with_capacity(segment_capacity)) {}
+
+durable_log::durable_log(const durable_log_options& options)
     : m_path()
     , m_dir(-1)
     , m_lock_fd(-1)
@@ -228,14 +318,15 @@ durable_log::durable_log(size_t segment_capacity)
     , m_error(0)
     , m_wakeup(false)
     , m_opened(false)
-    , m_capacity(segment_capacity ? segment_capacity : kDefaultCapacity)
+    , m_capacity(options.segment_capacity ? options.segment_capacity : kDefaultCapacity)
+    , m_opts(options)
     , m_segment_a(nullptr)
     , m_segment_b(nullptr)
     , m_active(nullptr)
     , m_durable(1)
     , m_flush_idle(false)
     , m_crc(gpu_batch)
-    , m_crc_ctx(nullptr)
+    , m_crc_ctx(&m_opts)
     , m_pinned(true)
     , m_flushes(0)
     , m_frames_flushed(0)
@@ -264,11 +355,12 @@ durable_log::~durable_log() throw()
         delete[] s->at;
         if (s->arena)
         {
-            if (m_pinned)
+            if (s->pinned)
                 mi_host_free_pinned(s->arena);
             else
                 free(s->arena);
         }
+        for (segment::External& x : s->ext) free(x.frame);
         delete s;
     }
     if (m_lock_fd >= 0) ::close(m_lock_fd);
@@ -280,7 +372,7 @@ void durable_log::set_batch_crc_for_testing(durable_log_batch_crc fn, void* ctx)
     std::lock_guard<std::mutex> hold(m_mtx);
     if (m_opened) return;
     m_crc = fn ? fn : gpu_batch;
-    m_crc_ctx = ctx;
+    m_crc_ctx = fn ? ctx : &m_opts;
     m_pinned = !fn;
 }
 
@@ -355,10 +447,11 @@ bool durable_log::open(const std::string& dir)
         segs[i]->fd = fds[i];
         segs[i]->cap = m_capacity;
         void* p = nullptr;
-        if (m_pinned)
-        {
-            if (mi_host_malloc_pinned(&p, m_capacity) != MI_CRC32C_OK) p = nullptr;
-        }
+        // pinned staging lets the GPU batch DMA the segment in place; without
+        // a usable device the log still works from ordinary memory (its CRCs
+        // then come from the engine's CPU path)
+        if (m_pinned && mi_host_malloc_pinned(&p, m_capacity) == MI_CRC32C_OK)
+            segs[i]->pinned = true;
         else
             p = malloc(m_capacity);
         segs[i]->arena = static_cast<unsigned char*>(p);
@@ -371,7 +464,7 @@ bool durable_log::open(const std::string& dir)
         m_error = ENOMEM;
         for (segment* s : segs)
         {
-            if (s->arena) m_pinned ? (void)mi_host_free_pinned(s->arena) : free(s->arena);
+            if (s->arena) s->pinned ? (void)mi_host_free_pinned(s->arena) : free(s->arena);
             delete[] s->at;
             ::close(s->fd);
             delete s;
@@ -394,14 +487,14 @@ void durable_log::close()
     std::unique_lock<std::mutex> hold(m_mtx);
     if (m_error == 0 && m_active.load())
     {
-        // Deviation (stronger than the reference): staged frames are flushed
-        // before the log shuts down, so close() never drops appended records.
-        m_cond.wait(hold, [&] {
-            if (m_error != 0) return true;
-            const segment* act = m_active.load();
-            const uint64_t w = act->word.load();
-            return m_durable.load() == act->base + ((w & ~kSealed) >> kIdxShift);
-        });
+        // Deviation (stronger than the reference, :172-177): every record
+        // reserved before close() was called is made durable before the log
+        // shuts down.  The bound is read once, so appenders that keep going
+        // cannot hold close() up; their later records may or may not be
+        // flushed, as with the reference, whose close() drops them all.
+        const segment* act = m_active.load();
+        const uint64_t ub = act->base + ((act->word.load() & ~kSealed) >> kIdxShift);
+        m_cond.wait(hold, [&] { return m_error != 0 || m_durable.load() >= ub; });
     }
     if (m_error == 0) m_error = -1;
     m_cond.notify_all();
@@ -414,7 +507,17 @@ int64_t durable_log::append(const char* entry, size_t entry_sz)
 
 int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
 {
+    if (entry_sz > UINT64_MAX - kHeader - kTrailer)
+    {
+        errno = EMSGSIZE;
+        return -1;
+    }
     const uint64_t frame = kHeader + entry_sz + kTrailer;
+    // Frames of more than half the staging arena are staged outside it
+    // (segment::External), so an entry of any size is accepted, as by the
+    // reference (txman/durable_log.cc:187-242).
+    const bool external = frame > m_capacity / 2;
+    const uint64_t arena_bytes = external ? 0 : frame;
     while (true)
     {
         if (const int e = m_error.load())
@@ -428,18 +531,13 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
             errno = EBADF;
             return -1;
         }
-        if (frame > m_capacity || entry_sz > UINT32_MAX - kHeader)
-        {
-            errno = EMSGSIZE;
-            return -1;
-        }
         // record number and staging offset in one step (txman/durable_log.cc:
         // 195-213 takes m_mtx for the same reservation)
-        const uint64_t w = seg->word.fetch_add((uint64_t(1) << kIdxShift) | frame);
+        const uint64_t w = seg->word.fetch_add((uint64_t(1) << kIdxShift) | arena_bytes);
         if (!(w & kSealed))
         {
             const uint64_t idx = w >> kIdxShift, at = w & kUsedMask;
-            if (at + frame <= seg->cap && idx < seg->slots)
+            if (at + arena_bytes <= seg->cap && idx < seg->slots)
             {
                 if (idx == 0 && m_flush_idle.load())
                 {
@@ -448,12 +546,36 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
                 }
                 // encode_header (txman/durable_log.cc:57-61) and the entry
                 const uint64_t recno = seg->base + idx;
-                unsigned char* p = seg->arena + at;
-                pack64be(recno, p);
-                pack64be(entry_sz, p + 8);
-                if (entry_sz) memcpy(p + kHeader, entry, entry_sz);
-                seg->at_slot(idx) = at;
+                unsigned char* p = external ? static_cast<unsigned char*>(malloc(frame))
+                                            : seg->arena + at;
+                if (p)
+                {
+                    pack64be(recno, p);
+                    pack64be(entry_sz, p + 8);
+                    if (entry_sz) memcpy(p + kHeader, entry, entry_sz);
+                }
+                if (external)
+                {
+                    // written in record order, just before the arena bytes
+                    // reserved after it (its slot holds that arena offset)
+                    std::lock_guard<std::mutex> hold(seg->ext_mu);
+                    seg->ext.push_back(segment::External{idx, p, p ? frame : 0});
+                    seg->at_slot(idx) = at | kExternal;
+                }
+                else
+                    seg->at_slot(idx) = at;
                 seg->done[done_shard()].n.fetch_add(1, std::memory_order_release);
+                if (!p)
+                {
+                    // out of memory for a record that already holds a record
+                    // number: fatal for the log, as an I/O error is in the
+                    // reference (txman/durable_log.cc:226-230)
+                    std::lock_guard<std::mutex> hold(m_mtx);
+                    if (m_error == 0) m_error = ENOMEM;
+                    m_cond.notify_all();
+                    errno = ENOMEM;
+                    return -1;
+                }
                 return int64_t(recno);
             }
             // Full.  `used` only grows, so every reservation from this one on
@@ -523,9 +645,37 @@ int durable_log::error()
     return m_error;
 }
 
-// Checksum the segment's n frames in one batch, patch the CRCs in and write
-// the staged bytes at the end of the file (the sync thread fsyncs it).  The
-// frames sit back to back from offset 0; their offsets come from the slots.
+// The batch CRC of n staged frames through the configured engine.  The
+// default engine completes engine failures on the CPU path itself; if an
+// injected test engine fails, the engine's CPU path completes the batch here
+// (counted in mi_crc32c_stats), so a failed checksum never fails the log.
+int durable_log::batch_crc(const unsigned char* base, const uint64_t* offs, const uint32_t* lens,
+                           size_t n, uint64_t total, uint32_t* out)
+{
+    if (m_crc(m_crc_ctx, base, offs, lens, n, total, out) == 0) return 0;
+    mi_host::batch(base, offs, lens, nullptr, n, out);
+    mi_host::note_fallback(MI_CRC32C_EHIP, total);
+    return 0;
+}
+
+// CRC of one frame's header + entry (`length` bytes) staged on its own.
+uint32_t durable_log::frame_crc(const unsigned char* frame, uint64_t length)
+{
+    if (m_crc != gpu_batch && length <= kBatchFrameMax)
+    {
+        const uint64_t off = 0;
+        const uint32_t len = uint32_t(length);
+        uint32_t c = 0;
+        batch_crc(frame, &off, &len, 1, length, &c);
+        return c;
+    }
+    return single_crc(frame, length);
+}
+
+// Checksum the segment's n frames -- the arena's in one batch, external ones
+// one by one -- patch the CRCs in and write the frames in record order at the
+// end of the file (the sync thread fsyncs it).  Arena frames sit back to
+// back from offset 0; their offsets come from the slots.
 int durable_log::write_segment(segment* seg, uint64_t n, uint64_t used)
 {
     auto t = std::chrono::steady_clock::now();
@@ -534,33 +684,70 @@ int durable_log::write_segment(segment* seg, uint64_t n, uint64_t used)
         m_flush_ns[phase] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(u - t).count());
         t = u;
     };
+    std::vector<segment::External> ext;
+    {
+        std::lock_guard<std::mutex> hold(seg->ext_mu);
+        ext.swap(seg->ext);
+    }
+    std::sort(ext.begin(), ext.end(),
+              [](const segment::External& x, const segment::External& y) { return x.idx < y.idx; });
+    // frames past the cut were never handed out (their appenders retried)
+    while (!ext.empty() && ext.back().idx >= n)
+    {
+        free(ext.back().frame);
+        ext.pop_back();
+    }
+    struct Release
+    {
+        std::vector<segment::External>& v;
+        ~Release()
+        {
+            for (segment::External& x : v) free(x.frame);
+        }
+    } release{ext};
     if (n)
     {
         m_offs.resize(n);
         m_lens.resize(n);
         m_crcs.resize(n);
-        uint64_t total = 0;
-        for (uint64_t i = 0; i < n; ++i) m_offs[i] = seg->at_slot(i);
+        uint64_t k = 0, total = 0;
         for (uint64_t i = 0; i < n; ++i)
         {
-            const uint64_t end = i + 1 < n ? m_offs[i + 1] : used;
+            const uint64_t a = seg->at_slot(i);
+            if (!(a & kExternal)) m_offs[k++] = a;
+        }
+        for (uint64_t i = 0; i < k; ++i)
+        {
+            const uint64_t end = i + 1 < k ? m_offs[i + 1] : used;
             if (end < m_offs[i] + kHeader + kTrailer) return EIO;  // offsets must tile the bytes
             m_lens[i] = uint32_t(end - m_offs[i] - kTrailer);
             total += m_lens[i];
         }
         lap(1);
-        if (m_crc(m_crc_ctx, seg->arena, m_offs.data(), m_lens.data(), size_t(n), total,
-                  m_crcs.data()) != 0)
-            return EIO;
+        if (k) batch_crc(seg->arena, m_offs.data(), m_lens.data(), size_t(k), total, m_crcs.data());
+        for (segment::External& x : ext)
+            if (x.frame)
+                pack32be(frame_crc(x.frame, x.bytes - kTrailer), x.frame + x.bytes - kTrailer);
         lap(2);
         // crc32c(crc32c(0, header, 16), entry) == crc32c(0, header || entry),
         // stored big-endian after the entry (txman/durable_log.cc:215-224)
-        for (uint64_t i = 0; i < n; ++i) pack32be(m_crcs[i], seg->arena + m_offs[i] + m_lens[i]);
+        for (uint64_t i = 0; i < k; ++i) pack32be(m_crcs[i], seg->arena + m_offs[i] + m_lens[i]);
         lap(3);
     }
-    if (used && !pwrite_all(seg->fd, seg->arena, used, off_t(seg->file_size))) return errno;
+    uint64_t at = 0, file = seg->file_size;
+    for (const segment::External& x : ext)
+    {
+        const uint64_t upto = seg->at_slot(x.idx) & ~kExternal;
+        if (upto > at && !pwrite_all(seg->fd, seg->arena + at, upto - at, off_t(file))) return errno;
+        file += upto - at;
+        at = upto;
+        if (x.bytes && !pwrite_all(seg->fd, x.frame, x.bytes, off_t(file))) return errno;
+        file += x.bytes;
+    }
+    if (used > at && !pwrite_all(seg->fd, seg->arena + at, used - at, off_t(file))) return errno;
+    file += used - at;
     lap(4);
-    seg->file_size += used;
+    seg->file_size = file;
     return 0;
 }
 
@@ -734,7 +921,9 @@ int64_t durable_log::replay(void (*f)(void*, const unsigned char*, size_t), void
     for (int i = 0; i < 2; ++i)
     {
         if (!read_file(dirfd, names[i], &bufs[i])) return -1;
-        if (scan_frames(bufs[i].data(), bufs[i].size(), fn, ctx, &frames[i], nullptr) < 0)
+        Chained ch{fn, ctx};
+        if (scan_frames(bufs[i].data(), bufs[i].size(), batch_or_host, &ch, single_crc,
+                        &frames[i], nullptr) < 0)
         {
             errno = EIO;
             return -1;
@@ -757,13 +946,24 @@ int64_t durable_log::replay(void (*f)(void*, const unsigned char*, size_t), void
 // ---- C ABI ------------------------------------------------------------------
 struct mi_dlog
 {
-    explicit mi_dlog(size_t cap) : log(cap) {}
+    explicit mi_dlog(const consus::durable_log_options& o) : log(o) {}
     durable_log log;
 };
 
 extern "C" {
 
-mi_dlog* mi_dlog_create(size_t segment_capacity) { return new mi_dlog(segment_capacity); }
+mi_dlog* mi_dlog_create(size_t segment_capacity)
+{
+    return new mi_dlog(with_capacity(segment_capacity));
+}
+mi_dlog* mi_dlog_create_ex(size_t segment_capacity, int gpus, uint64_t shard_min_bytes)
+{
+    consus::durable_log_options o;
+    o.segment_capacity = segment_capacity;
+    o.gpus = gpus;
+    o.shard_min_bytes = shard_min_bytes;
+    return new mi_dlog(o);
+}
 void mi_dlog_destroy(mi_dlog* l) { delete l; }
 int mi_dlog_open(mi_dlog* l, const char* dir)
 {
@@ -810,7 +1010,8 @@ int64_t mi_dlog_scan_file(const char* path, uint64_t* valid_bytes, uint64_t* rec
     std::vector<unsigned char> buf;
     if (!read_file(-1, path, &buf)) return -1;
     std::vector<Frame> frames;
-    const int64_t n = scan_frames(buf.data(), buf.size(), gpu_batch, nullptr, &frames, valid_bytes);
+    const int64_t n =
+        scan_frames(buf.data(), buf.size(), gpu_batch, nullptr, single_crc, &frames, valid_bytes);
     if (n < 0) return -1;
     for (size_t i = 0; i < frames.size() && i < max_frames; ++i)
     {

@@ -25,18 +25,13 @@
 #include "../../include/consus_crc32c.h"
 #include "crc32c_kernels.h"
 #include "crc32c_math.h"
+#include "engine_internal.h"
 
 using namespace mi_crc;
+using mi_eng::fail;
+using mi_eng::kMaxDevices;
 
 namespace {
-
-thread_local std::string t_err;
-
-int fail(int status, const std::string& msg)
-{
-    t_err = msg;
-    return status;
-}
 
 #define HIP_TRY(expr)                                                                     \
     do {                                                                                  \
@@ -65,20 +60,49 @@ struct DeviceState
 };
 
 std::mutex g_mu;
-std::atomic<DeviceState*> g_dev{nullptr};
+std::atomic<DeviceState*> g_devs[kMaxDevices];  // per ordinal, built on first use
+std::atomic<int> g_default{-1};                 // the process's default device
 
-int init_device(int device)
+// Fault injection for the fallback tests (read once): MI_CRC32C_FAULT=init
+// makes every device fail to initialise (as on a host without a usable GPU);
+// =compute initialises normally but fails every compute call with EHIP (a
+// HIP error at run time).  Unset in production.
+enum Fault { kFaultNone = 0, kFaultInit = 1, kFaultCompute = 2 };
+int fault_mode()
 {
-    std::lock_guard<std::mutex> lock(g_mu);
-    if (DeviceState* d = g_dev.load())
+    static const int mode = [] {
+        const char* e = std::getenv("MI_CRC32C_FAULT");
+        if (!e) return int(kFaultNone);
+        if (!std::strcmp(e, "init")) return int(kFaultInit);
+        if (!std::strcmp(e, "compute")) return int(kFaultCompute);
+        return int(kFaultNone);
+    }();
+    return mode;
+}
+
+bool is_gfx950(int device, std::string* arch = nullptr)
+{
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
     {
-        if (d->ordinal == device || device < 0) return MI_CRC32C_OK;
-        return fail(MI_CRC32C_EINVAL, "engine already initialised on another device");
+        (void)hipGetLastError();
+        return false;
     }
-    if (device < 0) device = 0;
+    if (arch) *arch = prop.gcnArchName;
+    return std::string(prop.gcnArchName).find("gfx950") != std::string::npos;
+}
+
+// Builds the operator tables of `device` (once per device); the caller holds g_mu.
+int build_device(int device)
+{
+    if (fault_mode() == kFaultInit)
+        return fail(MI_CRC32C_ENODEV, "fault injected (MI_CRC32C_FAULT=init)");
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= device)
+    if (device < 0 || device >= kMaxDevices || hipGetDeviceCount(&n) != hipSuccess || n <= device)
+    {
+        (void)hipGetLastError();
         return fail(MI_CRC32C_ENODEV, "no HIP device " + std::to_string(device));
+    }
     HIP_TRY(hipSetDevice(device));
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -90,7 +114,6 @@ int init_device(int device)
     d->ordinal = device;
     d->cus = prop.multiProcessorCount;
     d->arch = arch;
-
     // Operator-table image (crc32c_math.h): G^{128}, T_0..T_15, G^{32}, G^{64}, G^{4096}.
     std::vector<uint32_t> img(kTabWords);
     make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabMain]), kRowBytes);
@@ -154,17 +177,50 @@ int init_device(int device)
         delete d;
         return fail(MI_CRC32C_EHIP, std::string("table upload: ") + hipGetErrorString(e));
     }
-    g_dev.store(d);
+    g_devs[device].store(d);
     return MI_CRC32C_OK;
 }
 
-DeviceState* dev_or_init(int* status)
+// The state of `device` (-1 = the default device), initialised on first use.
+DeviceState* device_state(int device, int* status)
 {
-    DeviceState* d = g_dev.load();
-    if (d) return d;
-    *status = init_device(0);
-    return g_dev.load();
+    if (device < 0)
+    {
+        device = g_default.load();
+        if (device < 0)
+        {
+            std::lock_guard<std::mutex> lock(g_mu);
+            if (g_default.load() < 0) g_default.store(0);
+            device = g_default.load();
+        }
+    }
+    if (device >= kMaxDevices)
+    {
+        *status = fail(MI_CRC32C_ENODEV, "device ordinal " + std::to_string(device) + " >= 16");
+        return nullptr;
+    }
+    if (DeviceState* d = g_devs[device].load()) return d;
+    std::lock_guard<std::mutex> lock(g_mu);
+    if (DeviceState* d = g_devs[device].load()) return d;
+    *status = build_device(device);
+    return g_devs[device].load();
 }
+
+// mi_crc32c_init: the default device is chosen once per process.
+int init_device(int device)
+{
+    {
+        std::lock_guard<std::mutex> lock(g_mu);
+        const int cur = g_default.load();
+        if (cur >= 0 && device >= 0 && cur != device)
+            return fail(MI_CRC32C_EINVAL, "engine already initialised on another device");
+        if (cur < 0) g_default.store(device < 0 ? 0 : device);
+    }
+    int st = MI_CRC32C_OK;
+    return device_state(-1, &st) ? MI_CRC32C_OK : st;
+}
+
+DeviceState* dev_or_init(int* status) { return device_state(-1, status); }
 
 // Grow-only device buffer.
 struct DevBuf
@@ -237,10 +293,12 @@ struct Ctx
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     PinBuf pin_small;                   // plan-size read-back, small host outputs
     PinBuf pin_stage, pin_out;          // packed small host batches: inputs, CRCs
+    int ordinal = -1;
 
-    int open(int ordinal)
+    int open(int dev)
     {
-        HIP_TRY(hipSetDevice(ordinal));
+        ordinal = dev;
+        HIP_TRY(hipSetDevice(dev));
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreate(&ev0));
         HIP_TRY(hipEventCreate(&ev1));
@@ -266,28 +324,45 @@ struct Ctx
     }
 };
 
-// One context per calling thread, released when the thread exits (a durable
-// log's flush thread lives as long as the log is open; its workspaces go
-// with it).
+// One context per (calling thread, device), released when the thread exits
+// (a durable log's flush thread lives as long as the log is open; its
+// workspaces go with it; the multi-device workers of api.cc live as long as
+// the process).
 struct ThreadCtx
 {
-    Ctx* c = nullptr;
+    Ctx* c[kMaxDevices] = {};
+    int current = -1;  // the device this thread last made current
     ~ThreadCtx()
     {
-        if (c)
-        {
-            c->release();
-            delete c;
-        }
+        for (Ctx*& x : c)
+            if (x)
+            {
+                (void)hipSetDevice(x->ordinal);
+                x->release();
+                delete x;
+                x = nullptr;
+            }
     }
 };
 thread_local ThreadCtx t_ctx;
 
-Ctx* thread_ctx(int* status)
+// The calling thread's context on `dev` (-1 = default device); makes `dev`
+// the thread's current HIP device (allocations go there).
+Ctx* thread_ctx_on(int dev, DeviceState** dout, int* status)
 {
-    DeviceState* d = dev_or_init(status);
+    DeviceState* d = device_state(dev, status);
     if (!d) return nullptr;
-    if (t_ctx.c) return t_ctx.c;
+    if (dout) *dout = d;
+    if (t_ctx.current != d->ordinal)
+    {
+        if (hipSetDevice(d->ordinal) != hipSuccess)
+        {
+            *status = fail(MI_CRC32C_EHIP, "hipSetDevice(" + std::to_string(d->ordinal) + ")");
+            return nullptr;
+        }
+        t_ctx.current = d->ordinal;
+    }
+    if (Ctx* c = t_ctx.c[d->ordinal]) return c;
     auto* c = new Ctx;
     *status = c->open(d->ordinal);
     if (*status != MI_CRC32C_OK)
@@ -296,9 +371,11 @@ Ctx* thread_ctx(int* status)
         delete c;
         return nullptr;
     }
-    t_ctx.c = c;
+    t_ctx.c[d->ordinal] = c;
     return c;
 }
+
+Ctx* thread_ctx(int* status) { return thread_ctx_on(-1, nullptr, status); }
 
 bool is_pinned(const void* p)
 {
@@ -326,10 +403,10 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
             uint64_t max_len = UINT64_MAX)  // longest record if known (host batches)
 {
     if (count == 0) return MI_CRC32C_OK;
-    if (count >= (1ull << 31)) return fail(MI_CRC32C_EINVAL, "count >= 2^31 records");
+    if (count >= (1ull << 31)) return fail(MI_CRC32C_ERANGE, "count >= 2^31 records");
     // items pack addresses in 41 bits (crc32c_kernels.h: Item); user-space and
     // GPU virtual addresses are below 2^47
-    if (uintptr_t(base) >= (kItemMaxAddr >> 1)) return fail(MI_CRC32C_EINVAL, "address above 2^47");
+    if (uintptr_t(base) >= (kItemMaxAddr >> 1)) return fail(MI_CRC32C_ERANGE, "address above 2^47");
     // small batches of short records: one launch, no plan (a durable-log
     // flush, one host call); a team hashes a record's rows serially, so only
     // when the longest record is known to be short
@@ -349,7 +426,7 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
                                : std::max<uint64_t>(c->items.cap / sizeof(Item), 2 * count + 1);
     for (int attempt = 0; attempt < 2; ++attempt)
     {
-        if (cap >= (1ull << 32)) return fail(MI_CRC32C_EINVAL, "plan exceeds 2^32 chunks");
+        if (cap >= (1ull << 32)) return fail(MI_CRC32C_ERANGE, "plan exceeds 2^32 chunks");
         if ((st = c->items.reserve(cap * sizeof(Item))) || (st = c->partial.reserve(cap * 4)))
             return st;
         cap = std::min<uint64_t>(c->items.cap / sizeof(Item), c->partial.cap / 4);
@@ -418,22 +495,6 @@ extern "C" {
 
 int mi_crc32c_init(int device) { return init_device(device); }
 
-const char* mi_crc32c_strerror(int status)
-{
-    switch (status)
-    {
-        case MI_CRC32C_OK: return "ok";
-        case MI_CRC32C_EINVAL: return "invalid argument";
-        case MI_CRC32C_ENODEV: return "no usable gfx950 device";
-        case MI_CRC32C_ENOMEM: return "out of memory";
-        case MI_CRC32C_EHIP: return "HIP runtime error";
-        case MI_CRC32C_ERCCL: return "RCCL error";
-        default: return "unknown status";
-    }
-}
-
-const char* mi_crc32c_last_error(void) { return t_err.c_str(); }
-
 void* mi_crc32c_stream(void)
 {
     int st = 0;
@@ -450,16 +511,36 @@ int mi_crc32c_stream_sync(void)
     return MI_CRC32C_OK;
 }
 
-int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
-                    const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
-                    unsigned flags)
+}  // extern "C"
+
+namespace mi_eng {
+
+int usable_devices(int* ordinals, int max)
+{
+    if (fault_mode() == kFaultInit) return 0;
+    int n = 0, k = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        return 0;
+    }
+    for (int i = 0; i < n && i < kMaxDevices && k < max; ++i)
+        if (is_gfx950(i)) ordinals[k++] = i;
+    return k;
+}
+
+int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* lengths,
+          const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
+          unsigned flags)
 {
     if (count == 0) return MI_CRC32C_OK;
     if (!offsets || !lengths || !out) return fail(MI_CRC32C_EINVAL, "null array with count > 0");
+    if (fault_mode() == kFaultCompute)
+        return fail(MI_CRC32C_EHIP, "fault injected (MI_CRC32C_FAULT=compute)");
     int st = 0;
-    Ctx* c = thread_ctx(&st);
+    DeviceState* d = nullptr;
+    Ctx* c = thread_ctx_on(dev, &d, &st);
     if (!c) return st;
-    DeviceState* d = g_dev.load();
     if (flags & MI_CRC32C_DEVICE)
     {
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out))) return st;
@@ -565,8 +646,8 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
     return MI_CRC32C_OK;
 }
 
-int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
-                          const uint32_t* inits, size_t count, uint32_t* out, unsigned flags)
+int batch_fixed(int dev, const void* base, uint64_t stride, uint64_t length,
+                const uint32_t* inits, size_t count, uint32_t* out, unsigned flags)
 {
     if (count == 0) return MI_CRC32C_OK;
     if (!out || (!base && length)) return fail(MI_CRC32C_EINVAL, "null pointer with count > 0");
@@ -575,10 +656,12 @@ int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
     if (length && (__builtin_mul_overflow(uint64_t(count - 1), stride, &span) ||
                    __builtin_add_overflow(span, length, &span)))
         return fail(MI_CRC32C_EINVAL, "batch span overflows 64 bits");
+    if (fault_mode() == kFaultCompute)
+        return fail(MI_CRC32C_EHIP, "fault injected (MI_CRC32C_FAULT=compute)");
     int st = 0;
-    Ctx* c = thread_ctx(&st);
+    DeviceState* d = nullptr;
+    Ctx* c = thread_ctx_on(dev, &d, &st);
     if (!c) return st;
-    DeviceState* d = g_dev.load();
     if (flags & MI_CRC32C_DEVICE)
     {
         if ((st = run_fixed(d, c, base, stride, length, inits, count, out))) return st;
@@ -598,7 +681,7 @@ int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
     return MI_CRC32C_OK;
 }
 
-int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, unsigned flags)
+int buffer(int dev, uint32_t init, const void* data, size_t n, uint32_t* out, unsigned flags)
 {
     if (!out) return fail(MI_CRC32C_EINVAL, "null out");
     if (n == 0)
@@ -607,10 +690,12 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
         return MI_CRC32C_OK;
     }
     if (!data) return fail(MI_CRC32C_EINVAL, "null data");
+    if (fault_mode() == kFaultCompute)
+        return fail(MI_CRC32C_EHIP, "fault injected (MI_CRC32C_FAULT=compute)");
     int st = 0;
-    Ctx* c = thread_ctx(&st);
+    DeviceState* d = nullptr;
+    Ctx* c = thread_ctx_on(dev, &d, &st);
     if (!c) return st;
-    DeviceState* d = g_dev.load();
     // Device buffers of >= kSingleMin bytes (up to 64 GiB): launch_single.
     // Otherwise pieces of <= 16 MiB computed as one batch (one long-path record each,
     // so a 4 GiB buffer keeps 256 workgroups of long_finalize busy) and
@@ -618,7 +703,7 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
     // crc(0, B); init goes into piece 0.
     constexpr uint64_t kPiece = 16ull << 20;
     const size_t np = size_t((n + kPiece - 1) / kPiece);
-    if (np >= (1ull << 31)) return fail(MI_CRC32C_EINVAL, "buffer too large");
+    if (np >= (1ull << 31)) return fail(MI_CRC32C_ERANGE, "buffer too large");
     std::vector<uint64_t> off(np), after(np);
     std::vector<uint32_t> len(np), ini(np, 0), res(np);
     for (size_t i = 0; i < np; ++i)
@@ -673,7 +758,7 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
         *out = *h;
         return MI_CRC32C_OK;
     }
-    if ((st = mi_crc32c_batch(data, off.data(), len.data(), ini.data(), np, n, res.data(), 0)))
+    if ((st = batch(dev, data, off.data(), len.data(), ini.data(), np, n, res.data(), 0)))
         return st;
     uint32_t acc = 0;
     for (size_t i = 0; i < np; ++i) acc ^= apply_zeros(d, res[i], after[i]);
@@ -681,18 +766,9 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
     return MI_CRC32C_OK;
 }
 
-uint32_t mi_crc32c(uint32_t init, const void* data, size_t n)
-{
-    uint32_t out = 0;
-    const int st = mi_crc32c_buffer(init, data, n, &out, 0);
-    if (st != MI_CRC32C_OK)
-    {
-        std::fprintf(stderr, "consus_crc32c: GPU CRC-32C engine failed (%s): %s\n",
-                     mi_crc32c_strerror(st), t_err.c_str());
-        std::abort();
-    }
-    return out;
-}
+}  // namespace mi_eng
+
+extern "C" {
 
 uint32_t mi_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b)
 {
@@ -718,9 +794,9 @@ int mi_crc32c_combine_batch(const uint32_t* crc_a, const uint32_t* crc_b, const 
     if (count == 0) return MI_CRC32C_OK;
     if (!crc_a || !crc_b || !len_b || !out) return fail(MI_CRC32C_EINVAL, "null array");
     int st = 0;
-    Ctx* c = thread_ctx(&st);
+    DeviceState* d = nullptr;
+    Ctx* c = thread_ctx_on(-1, &d, &st);
     if (!c) return st;
-    DeviceState* d = g_dev.load();
     if (flags & MI_CRC32C_DEVICE)
     {
         HIP_TRY(launch_combine(crc_a, crc_b, len_b, count, out, d->d_pow2, c->stream));
@@ -754,6 +830,7 @@ struct mi_crc32c_pipeline
         size_t count = 0;
     };
     std::vector<Slot> slots;
+    DeviceState* dev = nullptr;  // the device the slots' streams and buffers live on
     size_t max_bytes = 0, max_records = 0;
     uint64_t next_ticket = 1;
     std::mutex mu;
@@ -785,6 +862,7 @@ int mi_crc32c_pipeline_create(size_t max_segment_bytes, size_t max_records, int 
     DeviceState* d = dev_or_init(&st);
     if (!d) return st;
     auto* p = new mi_crc32c_pipeline;
+    p->dev = d;
     p->slots.resize(size_t(depth));
     p->max_bytes = max_segment_bytes;
     p->max_records = max_records;
@@ -795,10 +873,12 @@ int mi_crc32c_pipeline_create(size_t max_segment_bytes, size_t max_records, int 
             (st = s.dseg.reserve(max_segment_bytes + 16)) ||
             (st = s.dmeta.reserve(max_records * 16)) || (st = s.ctx.out.reserve(max_records * 4)))
         {
+            t_ctx.current = -1;
             mi_crc32c_pipeline_destroy(p);
             return st;
         }
     }
+    t_ctx.current = -1;  // Ctx::open made the pipeline's device current
     *out = p;
     return MI_CRC32C_OK;
 }
@@ -821,7 +901,12 @@ int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, s
         maxlen = std::max<uint64_t>(maxlen, lengths[i]);
     }
     std::lock_guard<std::mutex> lock(p->mu);
-    DeviceState* d = g_dev.load();
+    DeviceState* d = p->dev;
+    if (t_ctx.current != d->ordinal)
+    {
+        HIP_TRY(hipSetDevice(d->ordinal));
+        t_ctx.current = d->ordinal;
+    }
     const uint64_t t = p->next_ticket++;
     auto& s = p->slots[t % p->slots.size()];
     int st;
@@ -884,8 +969,7 @@ int mi_dev_malloc(void** p, size_t bytes)
 {
     int st = 0;
     if (!p) return fail(MI_CRC32C_EINVAL, "null out pointer");
-    if (!dev_or_init(&st)) return st;
-    HIP_TRY(hipSetDevice(g_dev.load()->ordinal));
+    if (!thread_ctx(&st)) return st;  // makes the default device current
     if (hipMalloc(p, std::max<size_t>(bytes, 1)) != hipSuccess)
         return fail(MI_CRC32C_ENOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed");
     return MI_CRC32C_OK;

@@ -17,6 +17,7 @@ BATCH_CRC_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void
 
 _SIGS = {
     "mi_dlog_create": (C.c_void_p, [C.c_size_t]),
+    "mi_dlog_create_ex": (C.c_void_p, [C.c_size_t, C.c_int, C.c_uint64]),
     "mi_dlog_destroy": (None, [C.c_void_p]),
     "mi_dlog_open": (C.c_int, [C.c_void_p, C.c_char_p]),
     "mi_dlog_close": (None, [C.c_void_p]),
@@ -49,10 +50,13 @@ def _lib():
 
 
 class DurableLog:
-    def __init__(self, segment_capacity: int = 0, batch_crc=None):
+    def __init__(self, segment_capacity: int = 0, batch_crc=None, gpus: int = 0,
+                 shard_min: int = 0):
         """batch_crc: optional C function pointer (mi_dlog_batch_crc) used
-        instead of the GPU -- a test hook; must be set before open()."""
-        self._h = _lib().mi_dlog_create(segment_capacity)
+        instead of the GPU -- a test hook; must be set before open().
+        gpus / shard_min: consus::durable_log_options (devices one flush may
+        shard over, 0 = all usable; per-device share threshold, 0 = default)."""
+        self._h = _lib().mi_dlog_create_ex(segment_capacity, gpus, shard_min)
         self._keep = batch_crc
         if batch_crc is not None:
             _lib().mi_dlog_set_batch_crc_for_testing(self._h, C.cast(batch_crc, C.c_void_p), None)

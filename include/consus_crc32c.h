@@ -6,11 +6,13 @@
  * (common/crc32c.h:40-41, common/crc32c.cc:122-126): reflected CRC-32C
  * (Castagnoli, poly 0x82F63B78), `init` is a previous CRC *output* (pre- and
  * post-inverted), n == 0 returns init.  Results are bit-identical to the
- * reference on every input.  The checksums themselves are always computed by
- * the HIP kernels on the GPU; there is no CPU fallback.  If the engine cannot
- * run, status-returning calls return a negative status and the drop-in
- * `mi_crc32c` / `consus::crc32c` abort with a message (they cannot return an
- * error under the reference's signature).
+ * reference on every input.  The checksums are computed by the HIP kernels on
+ * the GPU.  The drop-in `mi_crc32c` / `consus::crc32c` is total, as the
+ * reference is: if the engine fails (no usable gfx950 device, a HIP error, an
+ * input beyond the engine's limits) the call is completed by the engine's own
+ * CPU path and counted in mi_crc32c_stats().  Status-returning calls return
+ * the failure, unless called with MI_CRC32C_FALLBACK on host memory, in which
+ * case they complete on the CPU path too (and count it).
  *
  * Plain C types only; the caller owns every buffer.  Pointers are host
  * pointers unless MI_CRC32C_DEVICE is passed, in which case every pointer
@@ -35,6 +37,8 @@ extern "C" {
 #define MI_CRC32C_ENOMEM (-12)  /* device or pinned allocation failed */
 #define MI_CRC32C_EHIP (-5)     /* a HIP runtime call failed; see mi_crc32c_last_error() */
 #define MI_CRC32C_ERCCL (-71)   /* an RCCL call failed */
+#define MI_CRC32C_ERANGE (-34)  /* input beyond the GPU engine's limits (>= 2^31 records,
+                                   device addresses >= 2^47, > 2^32 planned pieces) */
 
 /* ---- flags -------------------------------------------------------------- */
 #define MI_CRC32C_DEVICE 0x1u   /* pointer arguments are device pointers */
@@ -44,6 +48,10 @@ extern "C" {
                                    planned path (plan -> chunks -> finalize), even
                                    for a batch of short records small enough for
                                    the one-launch direct kernel (tests, tuning) */
+#define MI_CRC32C_FALLBACK 0x8u /* host memory only: if the GPU engine fails, complete the
+                                   call on the engine's CPU path (counted in
+                                   mi_crc32c_stats) instead of returning the failure.
+                                   Bad arguments (MI_CRC32C_EINVAL) still fail. */
 
 /* ---- engine ------------------------------------------------------------- */
 /* Select the device and upload the operator tables.  Idempotent; called
@@ -53,12 +61,29 @@ int mi_crc32c_init(int device);
 const char* mi_crc32c_strerror(int status);
 /* Message of the last failure on the calling thread ("" if none). */
 const char* mi_crc32c_last_error(void);
+/* Number of usable (gfx950) devices; does not initialise them. */
+int mi_crc32c_device_count(void);
 /* The HIP stream (hipStream_t) the calling thread's work is enqueued on. */
 void* mi_crc32c_stream(void);
 int mi_crc32c_stream_sync(void);
 
+/* Counters of the whole process.  The GPU parity tests assert that
+ * fallback_calls stays 0: they certify the HIP kernels, not the CPU path. */
+typedef struct mi_crc32c_stats_t
+{
+    uint64_t gpu_calls;           /* compute calls completed by the HIP kernels */
+    uint64_t fallback_calls;      /* calls (or shards) completed by the CPU path */
+    uint64_t fallback_bytes;      /* bytes the CPU path hashed */
+    uint64_t sharded_calls;       /* multi-device calls split over more than one range */
+    int32_t last_fallback_status; /* engine status that forced the last fallback (0: none) */
+    int32_t reserved;
+} mi_crc32c_stats_t;
+void mi_crc32c_stats(mi_crc32c_stats_t* out);
+void mi_crc32c_stats_reset(void);
+
 /* ---- the drop-in -------------------------------------------------------- */
-/* Same signature and semantics as consus::crc32c
+/* Same signature and semantics as consus::crc32c; never fails (engine failures
+ * complete on the CPU path, counted in mi_crc32c_stats).
  * replaces: uint32_t consus::crc32c(uint32_t init, const unsigned char* data, size_t n)
  *           common/crc32c.h:40-41, common/crc32c.cc:122-126 */
 uint32_t mi_crc32c(uint32_t init, const void* data, size_t n);
@@ -85,6 +110,36 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
 int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
                           const uint32_t* inits, size_t count, uint32_t* out, unsigned flags);
 
+/* ---- multi-device host batches ------------------------- */
+/* The batch is cut into contiguous record ranges of about equal bytes
+ * (mi_crc32c_balanced_ranges), one per device, and each range is staged over
+ * its own device's PCIe link and hashed there, concurrently (one persistent
+ * worker thread per extra device).  Only as many devices are used as keep
+ * every range >= shard_min_bytes (0 = the measured default, 16 MiB;
+ * env MI_CRC32C_SHARD_MIN overrides the default), so small batches stay on
+ * one device.  devices/ndev: the ordinals to use (a list may repeat an
+ * ordinal: two ranges on one device, two streams); devices NULL = the
+ * list in env MI_CRC32C_DEVICES ("0,1,2,3") if set, else the usable devices;
+ * ndev > 0 then caps how many are used, ndev <= 0 = all of them.  Host memory only: device-resident
+ * records are hashed where they live (mi_crc32c_batch with MI_CRC32C_DEVICE).
+ * Flags: MI_CRC32C_FALLBACK (per range), MI_CRC32C_PLANNED.
+ * replaces: the per-record crc32c calls of durable_log::append
+ *           (txman/durable_log.cc:215-218) for a whole flushed segment. */
+int mi_crc32c_batch_multi(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                          const uint32_t* inits, size_t count, uint64_t total_bytes,
+                          uint32_t* out, unsigned flags, const int* devices, int ndev,
+                          uint64_t shard_min_bytes);
+/* Fixed-stride records, equal record counts per device. */
+int mi_crc32c_batch_fixed_multi(const void* base, uint64_t stride, uint64_t length,
+                                const uint32_t* inits, size_t count, uint32_t* out,
+                                unsigned flags, const int* devices, int ndev,
+                                uint64_t shard_min_bytes);
+/* The split rule: bounds[0..k] with bounds[0] = 0, bounds[k] = count; range r
+ * = records [bounds[r], bounds[r+1]) ends at the first record whose inclusive
+ * prefix sum of lengths reaches ceil(total * r / k). */
+void mi_crc32c_balanced_ranges(const uint32_t* lengths, size_t count, int k, uint64_t total,
+                               size_t* bounds);
+
 /* crc32c(0, A || B) from crc_a = crc32c(0, A), crc_b = crc32c(0, B) and |B|
  * (the chaining identity of common/crc32c.cc:122-126).  Pure operator math. */
 uint32_t mi_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
@@ -94,10 +149,15 @@ int mi_crc32c_combine_batch(const uint32_t* crc_a, const uint32_t* crc_b, const 
 /* ---- streaming host segments (H2D -> CRC -> D2H overlapped) ------------- */
 /* A pipeline of `depth` slots, each with pinned staging for one segment of
  * up to max_segment_bytes and max_records records, on its own HIP stream.
- * submit() copies the segment into pinned staging, enqueues
- * H2D + kernels + D2H of the CRCs and returns a ticket; wait() blocks until
- * that ticket's CRCs are in host_out.  Submitting into a busy slot waits for
- * that slot's previous ticket first. */
+ * submit() enqueues H2D + kernels + D2H of the CRCs and returns a ticket;
+ * wait() blocks until that ticket's CRCs are in host_out.  Submitting into a
+ * busy slot waits for that slot's previous ticket first.
+ * Buffer ownership: a PAGEABLE host_segment is copied into the slot's pinned
+ * staging before submit() returns, so the caller may reuse it at once.  A
+ * PINNED host_segment (mi_host_malloc_pinned, hipHostMalloc) is DMA'd in place
+ * -- no extra copy, which is what makes a pinned producer fast -- so it must
+ * stay allocated and unmodified until wait(ticket) returns; the CRCs are of
+ * the bytes the DMA reads.  offsets/lengths/inits are copied by submit(). */
 typedef struct mi_crc32c_pipeline mi_crc32c_pipeline;
 int mi_crc32c_pipeline_create(size_t max_segment_bytes, size_t max_records, int depth,
                               mi_crc32c_pipeline** out);

@@ -17,8 +17,15 @@ extern "C" {
 typedef struct mi_dlog mi_dlog;
 
 /* segment_capacity: bytes of staged (not yet flushed) frames per segment file;
- * 0 = 64 MiB.  An append that does not fit waits for the segment's flush. */
+ * 0 = 64 MiB.  An append that does not fit waits for the segment's flush;
+ * frames larger than half of it are staged on their own (any entry size is
+ * accepted, as by the reference). */
 mi_dlog* mi_dlog_create(size_t segment_capacity);
+/* The same with the knobs of consus::durable_log_options: gpus = devices one
+ * flush may shard over (0 = every usable device, 1 = the default device
+ * only); shard_min_bytes = per-device share below which a flush uses fewer
+ * devices (0 = the engine's measured default). */
+mi_dlog* mi_dlog_create_ex(size_t segment_capacity, int gpus, uint64_t shard_min_bytes);
 void mi_dlog_destroy(mi_dlog* log);
 int mi_dlog_open(mi_dlog* log, const char* dir);           /* 1 = ok, 0 = failed (bool) */
 void mi_dlog_close(mi_dlog* log);

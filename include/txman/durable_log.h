@@ -40,16 +40,28 @@
 
 namespace consus {
 
-// CRC engine for a batch of frames (default: the GPU, mi_crc32c_batch).
+// CRC engine for a batch of frames (default: the GPU, mi_crc32c_batch_multi).
 typedef int (*durable_log_batch_crc)(void* ctx, const void* base, const uint64_t* offsets,
                                      const uint32_t* lengths, size_t count, uint64_t total_bytes,
                                      uint32_t* out);
+
+// Tuning knobs (the reference has none: txman/main.cc:84-117 parses only
+// daemon flags; these map onto the same flag style, e.g. --log-segment-mb).
+struct durable_log_options
+{
+    size_t segment_capacity = 0;   // bytes of staged frames per segment; 0 = 64 MiB
+    int gpus = 0;                  // devices one flush may shard over: 0 = every usable
+                                   // gfx950 device, 1 = the engine's default device only
+    uint64_t shard_min_bytes = 0;  // per-device share below which a flush stays on fewer
+                                   // devices; 0 = the engine's measured default (16 MiB)
+};
 
 class durable_log
 {
     public:
         durable_log();
         explicit durable_log(size_t segment_capacity);
+        explicit durable_log(const durable_log_options& options);
         ~durable_log() throw ();
 
     public:
@@ -89,6 +101,9 @@ class durable_log
         int64_t append_slow(segment* seg);
         void switch_to_next(segment* seg, uint64_t n);
         int write_segment(segment* seg, uint64_t nframes, uint64_t used);
+        int batch_crc(const unsigned char* base, const uint64_t* offs, const uint32_t* lens,
+                      size_t n, uint64_t total, uint32_t* out);
+        uint32_t frame_crc(const unsigned char* frame, uint64_t length);
 
     private:
         std::string m_path;
@@ -102,6 +117,7 @@ class durable_log
         bool m_wakeup;
         bool m_opened;
         size_t m_capacity;
+        durable_log_options m_opts;
         segment* m_segment_a;
         segment* m_segment_b;
         std::atomic<segment*> m_active;      // the segment appends reserve in

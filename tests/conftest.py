@@ -32,6 +32,19 @@ def reference():
     return Reference()
 
 
+@pytest.fixture(autouse=True)
+def _gpu_path_certified(request):
+    """Every GPU test certifies the HIP kernels: the engine's CPU path
+    (mi_crc32c_stats().fallback_calls) must not have run in this process.
+    Tests that exercise the fallback on purpose do it in a subprocess."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import consus_amd
+    st = consus_amd.stats()
+    assert st["fallback_calls"] == 0, f"CPU-path fallback ran during a GPU test: {st}"
+
+
 @pytest.fixture(scope="session")
 def engine():
     import consus_amd

@@ -1,6 +1,8 @@
 """The C-ABI library: loads without a GPU, exports every declared symbol,
-fails loudly (no CPU fallback) when no gfx950 device is present, and its
-host-side operator algebra (combine) agrees with the oracle."""
+its status-returning calls fail loudly when no gfx950 device is present
+(only the total drop-in and MI_CRC32C_FALLBACK calls complete on the CPU
+path, tests/test_fallback.py), and its host-side operator algebra (combine)
+agrees with the oracle."""
 import ctypes
 import os
 import re
@@ -33,10 +35,15 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
-def test_dropin_symbol_exported():
+def test_dropin_definition_is_hidden_in_the_executable():
+    """consus::crc32c is declared in Consus's hidden namespace (namespace.h:4-5):
+    the library exports only the C ABI, and the definition (crc32c_dropin.cc)
+    is linked into the executable, as tools/dropin_check shows."""
     lib = ctypes.CDLL(E.LIB_PATH)
-    # uint32_t consus::crc32c(uint32_t, const unsigned char*, size_t)
-    assert hasattr(lib, "_ZN6consus6crc32cEjPKhm")
+    assert not hasattr(lib, "_ZN6consus6crc32cEjPKhm")
+    out = __import__("subprocess").run(["nm", "-C", os.path.join(REPO, "tools", "dropin_check")],
+                                       capture_output=True, text=True, timeout=60).stdout
+    assert "consus::crc32c(unsigned int, unsigned char const*, unsigned long)" in out
 
 
 def test_combine_host_algebra(oracle):

@@ -127,14 +127,96 @@ def test_backpressure_small_capacity(make_log, tmp_path):
     assert len(log.replay()) == 200
 
 
-def test_oversized_entry_and_closed_log(make_log, tmp_path):
+def test_closed_log_refuses_appends(make_log, tmp_path):
     log = make_log(capacity=4096)
     assert log.open(str(tmp_path / "d"))
-    assert log.append(b"x" * 5000) == -1
     assert log.append(b"ok") == 1
     log.close()
     assert log.append(b"late") == -1
     assert log.error() != 0
+
+
+@pytest.mark.parametrize("capacity", [4096, 1 << 16])
+def test_oversized_entries_accepted_in_order(make_log, tmp_path, oracle, capacity):
+    """Entries of any size are accepted, as by the reference's append
+    (txman/durable_log.cc:187-242): frames larger than half the staging
+    capacity are staged on their own and written in record order between
+    the arena's frames, with reference framing and CRCs."""
+    rng = np.random.default_rng(capacity)
+    log = make_log(capacity=capacity)
+    assert log.open(str(tmp_path / "d"))
+    sizes = [10, 2 * capacity, 0, capacity // 2, 3 * capacity + 7, 100, capacity, 5,
+             capacity // 2 - 20, 2 * capacity]
+    entries = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    recnos = [log.append(e) for e in entries]
+    assert recnos == list(range(1, len(entries) + 1))
+    wait_durable(log, len(entries))
+    log.close()
+    assert log.replay() == entries
+    frames = []
+    for f in ("file_a", "file_b"):
+        frames += parse_frames(tmp_path / "d" / f)
+    frames.sort()
+    assert [fr[0] for fr in frames] == recnos
+    for (recno, entry, crc, hdr_entry), want in zip(frames, entries):
+        assert entry == want
+        assert crc == oracle.crc32c(0, hdr_entry)
+
+
+def test_oversized_entries_concurrent(make_log, tmp_path):
+    """Big and small appends from 4 threads into a small log: every record
+    replays in order with its own bytes."""
+    log = make_log(capacity=8192)
+    assert log.open(str(tmp_path / "d"))
+    got = {}
+
+    def worker(t):
+        rng = np.random.default_rng(100 + t)
+        for i in range(60):
+            n = int(rng.choice([16, 200, 5000, 20000]))
+            e = bytes([t]) + i.to_bytes(2, "big") + bytes(n)
+            r = log.append(e)
+            assert r > 0
+            got[r] = e
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    wait_durable(log, 240)
+    log.close()
+    assert sorted(got) == list(range(1, 241))
+    assert log.replay() == [got[r] for r in range(1, 241)]
+
+
+def test_close_with_concurrent_appenders(make_log, tmp_path):
+    """close() waits only for the records reserved before it was called, so
+    appenders that keep going cannot hold it up (the reference's close,
+    txman/durable_log.cc:172-177, returns at once)."""
+    log = make_log(capacity=1 << 15)
+    assert log.open(str(tmp_path / "d"))
+    stop = threading.Event()
+    before = []
+
+    def worker():
+        while not stop.is_set():
+            if log.append(b"y" * 300) < 0:
+                break
+    for _ in range(20):
+        before.append(log.append(b"x" * 100))
+    ts = [threading.Thread(target=worker) for _ in range(4)]
+    for t in ts:
+        t.start()
+    closer = threading.Thread(target=log.close)
+    closer.start()
+    closer.join(timeout=60)
+    closed = not closer.is_alive()
+    stop.set()
+    for t in ts:
+        t.join(timeout=60)
+    assert closed, "close() did not return while appenders kept going"
+    assert log.durable() > max(before)
+    assert log.append(b"late") == -1
 
 
 def test_wake_returns_wait(make_log, tmp_path):

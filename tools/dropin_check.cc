@@ -6,7 +6,10 @@
 //   * the check value and the n == 0 contract (common/crc32c.cc:122-126);
 //   * consus::durable_log open / append / wait / replay / close in a
 //     temporary directory, and the frame bytes on disk.
-// Prints "dropin ok" and exits 0, or names the first failed check and exits 1.
+// Prints "dropin ok gpu_calls=G fallback_calls=F" and exits 0, or names the
+// first failed check and exits 1.  Without a usable GPU every check must still
+// pass (the drop-in is total, as the reference is) with F > 0; on the GPU the
+// test asserts F == 0.
 // Built by consus_amd/csrc/Makefile; run by tests/test_dropin_cpp.py.
 #include <stdint.h>
 #include <stdio.h>
@@ -18,6 +21,7 @@
 #include <vector>
 
 #include "common/crc32c.h"
+#include "consus_crc32c.h"
 #include "txman/durable_log.h"
 
 namespace {
@@ -106,6 +110,10 @@ int main()
     for (const char* n : {"/log/file_a", "/log/file_b", "/log/LOCK"}) unlink((d + n).c_str());
     rmdir((d + "/log").c_str());
     rmdir(dir);
-    if (!g_fail) printf("dropin ok\n");
+    mi_crc32c_stats_t st;
+    mi_crc32c_stats(&st);
+    if (!g_fail)
+        printf("dropin ok gpu_calls=%llu fallback_calls=%llu\n",
+               (unsigned long long)st.gpu_calls, (unsigned long long)st.fallback_calls);
     return g_fail;
 }
