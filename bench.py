@@ -26,8 +26,10 @@ The JSON line also carries
                 reports half of wide streaming reads, MI355X_MICROARCH.md HBM)
   cpu_baseline  the reference common/crc32c.cc itself (oracle/_ref, compiled
                 unmodified) on the host cores, over a bounded sample of the
-                same records (rank 0, N=1 only): its dispatched path single-
-                threaded and on up to 16 threads, and its slicing-by-8 path once
+                same records (rank 0, N=1 only): its dispatched path on every
+                CPU this process may use (min of affinity and cgroup quota,
+                both reported with nproc and the model), a 1/4/16/all-thread
+                sweep, and its slicing-by-8 path once
 
 Other workloads (--config, one JSON line each; see --help): zipf
 (configs[2]; at N > 1 sharded by bytes across the GPUs), single (one 4 GiB device record; at N > 1 one record split
@@ -195,53 +197,93 @@ def rccl_gather(E, dist, rank: int, world: int, out, R: int, digests, rec) -> di
 
 
 # ---- CPU baseline: the reference itself ---------------------------------------
+def host_cpus() -> dict:
+    """What this process may run on: the machine's CPUs (nproc), this
+    process's affinity mask, the cgroup CPU quota (cpu.max), and the model."""
+    info = {"nproc": os.cpu_count() or 1,
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+            else os.cpu_count() or 1,
+            "cgroup_quota_cpus": None, "model": ""}
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and parts and parts[0] != "max":
+            info["cgroup_quota_cpus"] = round(int(parts[0]) / int(parts[1]), 2)
+        elif path.endswith("quota_us") and parts and int(parts[0]) > 0:
+            try:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    info["cgroup_quota_cpus"] = round(int(parts[0]) / int(f.read()), 2)
+            except OSError:
+                pass
+        break
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return info
+
+
 def cpu_baseline(args) -> dict:
+    """The reference common/crc32c.cc itself (oracle/_ref, compiled unmodified)
+    over a bounded sample of the same records, on every CPU this process may
+    use: threads = min(affinity, cgroup quota) -- nothing is capped by a
+    constant.  A 1 / 4 / 16 / all-thread sweep goes with it."""
     from oracle.oracle import Oracle, Reference, reference_available
+    cpus = host_cpus()
     if not reference_available():
         return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference",
-                "sample": "oracle/_ref/libref_crc32c.so not built"}
+                "sample": "oracle/_ref/libref_crc32c.so not built", "host": cpus}
     ref, orc = Reference(), Oracle()
     L = args.record_bytes
     # 1 GiB sample of the same records: 4x the 256 MB L3 of the EPYC hosts, so
     # the CPU streams from DRAM as the GPU streams from HBM
     n = (1 << 30) // L
     buf = orc.fill(n * L, SEED, 0)
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
-                         else os.cpu_count() or 1))
+    usable = cpus["affinity"]
+    if cpus["cgroup_quota_cpus"]:
+        usable = max(1, min(usable, int(cpus["cgroup_quota_cpus"])))
 
-    def rate(th):
+    def rate(th, seconds):
+        ref.fixed(buf, L, L, n, threads=th)  # warm: thread start-up, caches, clocks
         passes, t0 = 0, time.perf_counter()
         while True:
             ref.fixed(buf, L, L, n, threads=th)
             passes += 1
             dt = time.perf_counter() - t0
-            if dt >= args.cpu_seconds:
+            if dt >= seconds:
                 return passes * n * L / dt / 2**30, passes
     crc_ref = ref.fixed(buf, L, L, 64, threads=1)
-    single, p1 = rate(1)
-    multi, pm = rate(threads)
+    leg = args.cpu_seconds / 2
+    sweep = {}
+    for th in sorted({1, 4, 16, usable} | ({cpus["affinity"]} if cpus["affinity"] <= 256 else set())):
+        if th > cpus["affinity"]:
+            continue
+        sweep[str(th)] = round(rate(th, leg)[0], 2)
+    multi, pm = rate(usable, args.cpu_seconds)
+    single = sweep["1"]
     # the reference's other path, slicing-by-8 (common/crc32c.cc:40-48, 594-634;
     # taken on CPUs without SSE4.2), once over 256 MiB of the sample
     t0 = time.perf_counter()
     ref.crc32c(0, buf, 256 << 20, impl="sw")
     sb8 = (256 << 20) / (time.perf_counter() - t0) / 2**30
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": round(multi, 2), "unit": "GiB/s", "cores": threads, "kind": "reference",
-            "single_thread_value": round(single, 2),
+    return {"value": round(multi, 2), "unit": "GiB/s", "cores": usable, "kind": "reference",
+            "single_thread_value": single,
             "slicing_by_8_single_thread_value": round(sb8, 2),
+            "thread_sweep_gib_s": sweep,
+            "host": cpus,
             "sample": f"first {n} of the same {L}-B records ({n * L >> 20} MiB, host DRAM), "
                       f"consus::crc32c from common/crc32c.cc compiled unmodified "
                       f"(dispatch {'sse42 crc32q' if ref.lib.ref_dispatch_is_sse42() else 'slicing-by-8'}), "
-                      f"{p1} passes single-thread + {pm} passes x {threads} std::threads, "
-                      f"cpu: {model}",
+                      f"{pm} passes x {usable} std::threads (= min(affinity {cpus['affinity']}, "
+                      f"cgroup quota {cpus['cgroup_quota_cpus']}); nproc {cpus['nproc']}), "
+                      f"cpu: {cpus['model']}",
             "first_crc": int(crc_ref[0])}
 
 

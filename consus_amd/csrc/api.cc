@@ -47,12 +47,14 @@ namespace {
 
 using mi_eng::fail;
 
-// Per-shard amortisation threshold of the multi-device entry points: a shard
-// costs one hand-off to a worker thread and one more staged host batch
-// (measured on MI355X, profiles/r02_shard_overhead.txt: ~30-60 us beside
-// ~52 GiB/s of pinned H2D per device), so a second device pays once each
-// shard carries >= ~16 MiB.  MI_CRC32C_SHARD_MIN (bytes) overrides it.
-constexpr uint64_t kShardMinDefault = uint64_t(16) << 20;
+// Per-range amortisation threshold of the multi-device entry points.
+// Measured on MI355X (tools/shard_probe.py, profiles/r02_shard_overhead.txt):
+// a host batch of 4 KiB records costs 0.114 / 0.157 / 0.424 / 1.28 ms on one
+// device at 1 / 4 / 16 / 64 MiB (pageable memory, 52-56 GB/s from 64 MiB up),
+// and the split itself (worker hand-off, a second stream and staging) adds
+// 2-15 us.  A range of >= 4 MiB therefore carries >= 0.157 ms of link time,
+// of which a split costs < 10 %.  MI_CRC32C_SHARD_MIN (bytes) overrides it.
+constexpr uint64_t kShardMinDefault = uint64_t(4) << 20;
 
 uint64_t shard_min(uint64_t arg)
 {

@@ -115,7 +115,7 @@ int mi_crc32c_batch_fixed(const void* base, uint64_t stride, uint64_t length,
  * (mi_crc32c_balanced_ranges), one per device, and each range is staged over
  * its own device's PCIe link and hashed there, concurrently (one persistent
  * worker thread per extra device).  Only as many devices are used as keep
- * every range >= shard_min_bytes (0 = the measured default, 16 MiB;
+ * every range >= shard_min_bytes (0 = the measured default, 4 MiB;
  * env MI_CRC32C_SHARD_MIN overrides the default), so small batches stay on
  * one device.  devices/ndev: the ordinals to use (a list may repeat an
  * ordinal: two ranges on one device, two streams); devices NULL = the

@@ -53,7 +53,7 @@ struct durable_log_options
     int gpus = 0;                  // devices one flush may shard over: 0 = every usable
                                    // gfx950 device, 1 = the engine's default device only
     uint64_t shard_min_bytes = 0;  // per-device share below which a flush stays on fewer
-                                   // devices; 0 = the engine's measured default (16 MiB)
+                                   // devices; 0 = the engine's measured default (4 MiB)
 };
 
 class durable_log

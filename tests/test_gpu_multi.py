@@ -52,9 +52,9 @@ def test_batch_multi_forced_split_parity(engine, oracle, devices):
 
 
 def test_batch_multi_threshold_keeps_small_batches_whole(engine, oracle):
-    buf, off, ln = zipf_batch(2000)
+    buf, off, ln = zipf_batch(500)  # ~2.3 MB: below one range's worth
     before = engine.stats()["sharded_calls"]
-    got = engine.crc32c_batch_multi(buf, off, ln, devices=[0, 0, 0])  # default 16 MiB per range
+    got = engine.crc32c_batch_multi(buf, off, ln, devices=[0, 0, 0])  # default 4 MiB per range
     assert np.array_equal(got, oracle.batch(buf, off, ln))
     assert engine.stats()["sharded_calls"] == before
     got = engine.crc32c_batch_multi(buf, off, ln)  # every usable device
@@ -62,8 +62,8 @@ def test_batch_multi_threshold_keeps_small_batches_whole(engine, oracle):
 
 
 def test_fixed_multi_large_host_batch(engine, oracle):
-    """256 MiB of 4 KiB records in host memory over 4 ranges (default
-    threshold: 64 MiB each), equal record counts per range."""
+    """256 MiB of 4 KiB records in host memory over 4 ranges (64 MiB each,
+    above the default threshold), equal record counts per range."""
     n = 65536
     buf = oracle.fill(n * 4096, 0xC0DE, 0)
     before = engine.stats()["sharded_calls"]
