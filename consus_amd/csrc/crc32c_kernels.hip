@@ -277,11 +277,27 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_kernel(
 }
 
 // Software-pipelined fast path for records of exactly G KiB (G even), the
-// shape of the headline batch (4 KiB): group g+1 -- or the next record's group
-// 0 -- is in flight while group g is folded, so every wave always has 8 KiB
-// of loads outstanding.  The loop body is straight-line per record, so the
-// loop-carried buffer is the same 8 loads on every path into the header and
-// the compiler's vmcnt accounting stays exact.
+// shape of the headline batch (4 KiB).  A record's rows are loaded in
+// sub-groups of Q rows into NB rotating buffers: NB - 1 sub-groups (of this
+// record or the next one) are in flight while one is folded, so a wave
+// always has (NB - 1) * Q KiB of loads outstanding, Q * NB rows of buffer
+// VGPRs.  The loop body is straight-line per record and every buffer's role
+// is the same in every record (NB divides the sub-groups per record), so the
+// loop-carried loads are the same on every path into the header and the
+// compiler's vmcnt accounting stays exact.
+// Shape (MI355X, 1M x 4 KiB, tools/ab.py, 6 interleaved rounds per build,
+// medians): Q = 1 row, NB = 4 (71 VGPRs) 0.640-0.648 ms; Q = 1, NB = 8
+// 0.642-0.648; Q = 1, NB = 2 0.645-0.652; Q = 2, NB = 4 0.651-0.657; Q = 4,
+// NB = 4 0.655-0.666; the former Q = 8, NB = 2 (two 8-row groups, 126 VGPRs)
+// 0.652-0.669.  Issuing one row ahead of each row's folding spreads the loads
+// evenly through the lookups; the depth beyond 3 rows changes nothing.
+// Dropping the sched_barrier costs 1 % (Q = 1, NB = 4: 0.649-0.655).
+#ifndef MI_PIPE_ROWS
+#define MI_PIPE_ROWS 1
+#endif
+#ifndef MI_PIPE_BUFS
+#define MI_PIPE_BUFS 4
+#endif
 template <int G, bool INITS>
 __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uint64_t stride,
                                            const uint32_t* __restrict__ inits,
@@ -289,7 +305,9 @@ __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uin
                                            uint32_t* __restrict__ out,
                                            const uint32_t* __restrict__ tables)
 {
-    static_assert(G % 2 == 0, "buffers alternate per group");
+    constexpr int Q = MI_PIPE_ROWS, NB = MI_PIPE_BUFS;
+    constexpr int SG = G * kGroupRows / Q;  // sub-groups per record
+    static_assert(G * kGroupRows % Q == 0 && SG % NB == 0 && NB >= 2, "pipeline shape");
     stage_tables(tables);
 
     const uint32_t tl = threadIdx.x & (kTeam - 1);
@@ -304,40 +322,42 @@ __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uin
         const uint64_t r = team + it * nteams;
         return r < count ? r : count - 1;
     };
-    auto load_group = [&](uint4 (&buf)[kGroupRows], uint64_t rec, int g) {
-        const uint8_t* p = base + rec * stride + tl * 16 + g * kGroupBytes;
+    auto load_sub = [&](uint4 (&buf)[Q], uint64_t rec, int q) {
+        const uint8_t* p = base + rec * stride + tl * 16 + q * Q * kRowBytes;
 #pragma unroll
-        for (int r = 0; r < kGroupRows; ++r) buf[r] = load16(p + r * kRowBytes);
+        for (int r = 0; r < Q; ++r) buf[r] = load16(p + r * kRowBytes);
     };
 
-    uint4 A[kGroupRows], B[kGroupRows];
+    uint4 bufs[NB][Q];
     uint64_t rec = rec_of(0);
     uint32_t init_word = INITS ? inits[rec * init_stride] : 0u;
-    load_group(A, rec, 0);
+#pragma unroll
+    for (int q = 0; q < NB - 1; ++q) load_sub(bufs[q], rec, q);
     for (uint64_t it = 0; it < iters; ++it)
     {
         const uint64_t next = rec_of(it + 1);
         uint32_t V[4] = {0, 0, 0, 0};
         uint32_t next_init = 0;
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+        for (int q = 0; q < SG; ++q)
         {
-            uint4(&cur)[kGroupRows] = (g % 2 == 0) ? A : B;
-            uint4(&nxt)[kGroupRows] = (g % 2 == 0) ? B : A;
-            if (g + 1 < G)
-                load_group(nxt, rec, g + 1);
+            const int qa = q + NB - 1;  // the sub-group issued now
+            if (qa < SG)
+                load_sub(bufs[qa % NB], rec, qa);
             else
             {
-                load_group(nxt, next, 0);
-                if (INITS) next_init = inits[next * init_stride];
+                load_sub(bufs[qa % NB], next, qa - SG);
+                if (INITS && qa == SG) next_init = inits[next * init_stride];
             }
-            // Keep all 8 loads ahead of this group's folding (the scheduler
+            // Keep the loads ahead of this sub-group's folding (the scheduler
             // would otherwise sink them into it to save registers).
+#ifndef MI_PIPE_NOSB
             __builtin_amdgcn_sched_barrier(0);
-
-            if (g == 0) cur[0].x ^= tl == 0 ? ~init_word : 0u;
+#endif
+            uint4(&cur)[Q] = bufs[q % NB];
+            if (q == 0) cur[0].x ^= tl == 0 ? ~init_word : 0u;
 #pragma unroll
-            for (int r = 0; r < kGroupRows; ++r) row_update(V, cur[r], li);
+            for (int r = 0; r < Q; ++r) row_update(V, cur[r], li);
         }
         const uint32_t raw = team_fold(V);
         if (tl == 0 && team + it * nteams < count) out[rec] = ~raw;

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 args = sys.argv[1:]
 zipf = "--zipf" in args
 libs = [a for a in args if a != "--zipf"]
-for rnd in range(3):
+for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
     for lib in libs:
         cmd = [sys.executable, os.path.join(HERE, "zipf_probe.py"), lib] if zipf else \
               [sys.executable, os.path.join(HERE, "perf_probe.py"), str(1 << 20), lib]
