@@ -977,6 +977,87 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
     }
 }
 
+#ifndef MI_CHUNK_RING
+#define MI_CHUNK_RING 8  // bit G-1: the bins of G groups that take the row ring
+#endif
+// The same work with the fixed kernel's row pipeline (fixed_pipe, Q = 1,
+// NB = 4): each row is issued three rows ahead of its folding, across item
+// boundaries (the next item's first rows are issued during this item's last
+// rows), descriptors two items ahead.  Every item has 8 G rows, a multiple of
+// the ring, so every buffer's role is the same in every item and vmcnt stays
+// exact.
+#ifndef MI_CHUNK_RING_NB4
+#define MI_CHUNK_RING_NB4 8  // ring depth of the 4-group bin (its 4 lead waves per CU need depth)
+#endif
+template <int G>
+__device__ __forceinline__ void chunk_bin_ring(const Item* __restrict__ items, uint32_t lo,
+                                               uint32_t hi, uint32_t* __restrict__ partial,
+                                               uint32_t team, uint32_t team0, uint32_t nteams,
+                                               uint32_t tl, uint32_t li, const uint8_t* zero16)
+{
+    if (hi <= lo || lo + team0 >= hi) return;
+    constexpr int RR = G * kGroupRows, NB = G == 4 ? MI_CHUNK_RING_NB4 : 4, AHEAD = NB - 1;
+    static_assert(RR % NB == 0, "ring roles per item");
+    const uint32_t iters = (hi - lo - team0 + nteams - 1) / nteams;
+    auto idx_of = [&](uint32_t k) {
+        const uint32_t i = lo + team + k * nteams;
+        return i < hi ? i : hi - 1;
+    };
+    // group-0 blocks wholly before the piece read a zero block
+    auto row_ptr = [&](const ChunkView& v, int r) {
+        const int32_t o = r * int32_t(kRowBytes);
+        return (r < kGroupRows && v.x + o <= -16) ? zero16 : v.p0 + o;
+    };
+    uint4 buf[NB];
+    ChunkView cur = view_of<G>(items[idx_of(0)], tl);
+    Item nit = items[idx_of(1)];
+#pragma unroll
+    for (int r = 0; r < AHEAD; ++r) buf[r] = load16(row_ptr(cur, r));
+    for (uint32_t k = 0; k < iters; ++k)
+    {
+        const Item nnit = items[idx_of(k + 2)];
+        const ChunkView nxt = view_of<G>(nit, tl);
+        uint32_t V[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < RR; ++r)
+        {
+            const int ra = r + AHEAD;
+            buf[ra % NB] = load16(ra < RR ? row_ptr(cur, ra) : row_ptr(nxt, ra - RR));
+            __builtin_amdgcn_sched_barrier(0);
+            uint4 d = buf[r % NB];
+            if (r < kGroupRows)
+            {
+                // rows before every team's piece leave V = 0: skip them
+                // (one-group pieces are sorted by row count, so this is common)
+                if (G == 1 && !__builtin_amdgcn_ballot_w64(cur.x + r * int32_t(kRowBytes) > -16))
+                    continue;
+                const bool start_here = (cur.rsb >> 4) == r;
+                if (__builtin_amdgcn_ballot_w64(start_here))
+                    d = mask_from(d, start_here ? (cur.rsb & 15) : 0);
+            }
+            if (r == RR - 1) d = mask_below(d, cur.ce);
+            row_update(V, d, li);
+        }
+        const uint32_t raw = team_fold(V);
+        const uint32_t i = lo + team + k * nteams;
+        if (tl == 0 && i < hi) partial[i] = raw;
+        cur = nxt;
+        nit = nnit;
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void chunk_bin_any(const Item* __restrict__ items, uint32_t lo,
+                                              uint32_t hi, uint32_t* __restrict__ partial,
+                                              uint32_t team, uint32_t team0, uint32_t nteams,
+                                              uint32_t tl, uint32_t li, const uint8_t* zero16)
+{
+    if (MI_CHUNK_RING & (1 << (G - 1)))
+        chunk_bin_ring<G>(items, lo, hi, partial, team, team0, nteams, tl, li, zero16);
+    else
+        chunk_bin<G>(items, lo, hi, partial, team, team0, nteams, tl, li, zero16);
+}
+
 // All bins in one launch with wave roles.  Measured on config 3 (MI355X):
 // the 4-group pieces are HBM-bound and reach the same rate with 4 waves per
 // CU as with 16, while the short pieces are bound by per-item latency and
@@ -1027,16 +1108,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
     {
         const uint32_t team = (blockIdx.x * lead + wave) * kTeam + tw;
         const uint32_t nteams = gridDim.x * lead * kTeam;
-        chunk_bin<4>(items, b0, split, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin_any<4>(items, b0, split, partial, team, team & ~7u, nteams, tl, li, zero16);
     }
     else
     {
         const uint32_t rest = 16u - lead;
         const uint32_t team = (blockIdx.x * rest + (wave - lead)) * kTeam + tw;
         const uint32_t nteams = gridDim.x * rest * kTeam;
-        chunk_bin<3>(items, b1, b2, partial, team, team & ~7u, nteams, tl, li, zero16);
-        chunk_bin<2>(items, b2, b3, partial, team, team & ~7u, nteams, tl, li, zero16);
-        chunk_bin<1>(items, b3, n_items, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin_any<3>(items, b1, b2, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin_any<2>(items, b2, b3, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin_any<1>(items, b3, n_items, partial, team, team & ~7u, nteams, tl, li, zero16);
     }
     // one relaxed atomic per wave grab; every wave leaves once the pool is empty
     while (split < b1)
@@ -1047,7 +1128,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
                                          __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t lo = split + __builtin_amdgcn_readfirstlane(got);
         if (lo >= b1) break;
-        chunk_bin<4>(items, lo, min(lo + kGrab, b1), partial, tw, 0u, 64u / kTeam, tl, li, zero16);
+        chunk_bin_any<4>(items, lo, min(lo + kGrab, b1), partial, tw, 0u, 64u / kTeam, tl, li, zero16);
     }
 }
 

@@ -6,7 +6,7 @@
 # script stops at the first failure.  Output: gpurun_out/prof_<TAG>/.
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-TAG="${1:-r01}"
+TAG="${1:-r02}"
 OUT="$ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -31,6 +31,7 @@ run bench_single 300 python bench.py --config single --no-cpu
 run bench_stream 300 python bench.py --config stream --no-cpu
 run bench_pcie4k 300 python bench.py --config pcie4k --no-cpu
 run bench_dlog 300 python bench.py --config dlog --steps 30
+run shard_overhead 300 python tools/shard_probe.py
 stats fixed4k
 stats zipf
 stats single
