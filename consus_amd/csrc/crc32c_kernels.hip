@@ -978,7 +978,7 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
 }
 
 #ifndef MI_CHUNK_RING
-#define MI_CHUNK_RING 8  // bit G-1: the bins of G groups that take the row ring
+#define MI_CHUNK_RING 0  // bit G-1: the bins of G groups that take the row ring (measured: none)
 #endif
 // The same work with the fixed kernel's row pipeline (fixed_pipe, Q = 1,
 // NB = 4): each row is issued three rows ahead of its folding, across item
