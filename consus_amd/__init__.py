@@ -36,6 +36,7 @@ FLAG_DEVICE = 0x1
 FLAG_ASYNC = 0x2
 FLAG_PLANNED = 0x4  # force plan -> chunks -> finalize (no one-launch direct kernel)
 FLAG_FALLBACK = 0x8  # host memory: complete on the engine's CPU path if the GPU fails (counted)
+FLAG_PACKED = 0x10  # device batches: records back to back in address order (stream path)
 ERANGE = -34
 MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D = 1, 2, 3
 
@@ -109,6 +110,7 @@ class Stats(C.Structure):
     """mi_crc32c_stats_t (include/consus_crc32c.h)."""
     _fields_ = [("gpu_calls", C.c_uint64), ("fallback_calls", C.c_uint64),
                 ("fallback_bytes", C.c_uint64), ("sharded_calls", C.c_uint64),
+                ("stream_batches", C.c_uint64),
                 ("last_fallback_status", C.c_int32),
                 ("reserved", C.c_int32)]
 
@@ -188,7 +190,7 @@ def crc32c_dropin(init_crc: int, data) -> int:
 
 
 def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False,
-                 fallback: bool = False) -> np.ndarray:
+                 fallback: bool = False, packed: bool = False) -> np.ndarray:
     """Per-record CRCs of host records [buf + off, +len)."""
     a = _as_u8(buf)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -202,7 +204,8 @@ def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False,
     _check(lib().mi_crc32c_batch(C.c_void_p(a.ctypes.data), _np_ptr(off), _np_ptr(ln),
                                  _np_ptr(ini), off.size, int(ln.sum(dtype=np.uint64)),
                                  _np_ptr(out), (FLAG_PLANNED if planned else 0) |
-                                 (FLAG_FALLBACK if fallback else 0)), "mi_crc32c_batch")
+                                 (FLAG_FALLBACK if fallback else 0) |
+                                 (FLAG_PACKED if packed else 0)), "mi_crc32c_batch")
     return out
 
 
@@ -349,8 +352,8 @@ def device_batch_fixed(data: DeviceBuffer, stride: int, length: int, count: int,
 
 def device_batch(data: DeviceBuffer, offsets: DeviceBuffer, lengths: DeviceBuffer, count: int,
                  out: DeviceBuffer, inits: DeviceBuffer | None = None, total_bytes: int = 0,
-                 asynchronous: bool = False) -> None:
-    flags = FLAG_DEVICE | (FLAG_ASYNC if asynchronous else 0)
+                 asynchronous: bool = False, packed: bool = False) -> None:
+    flags = FLAG_DEVICE | (FLAG_ASYNC if asynchronous else 0) | (FLAG_PACKED if packed else 0)
     _check(lib().mi_crc32c_batch(C.c_void_p(data.ptr), C.c_void_p(offsets.ptr),
                                  C.c_void_p(lengths.ptr),
                                  None if inits is None else C.c_void_p(inits.ptr), count,

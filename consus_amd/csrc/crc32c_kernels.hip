@@ -20,6 +20,8 @@
 // No MFMA: this is a GF(2) scan; the bound is HBM read bandwidth.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "crc32c_kernels.h"
 
 // Ablation modes for tools/ablate.py (the product build is mode 0):
@@ -1721,6 +1723,404 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Sorted batches as one stream.  When the records
+// are in address order and do not overlap -- offsets[i + 1] >= offsets[i] +
+// lengths[i]: a durable-log segment (frames with their 4-byte CRC slots
+// between them), BASELINE configs[2] -- the batch lies in the byte range
+// [lo, lo + span) with lo = base + offsets[0], and is hashed as the aligned
+// 4 KiB chunks that cover it, exactly as the headline kernel hashes 4 KiB
+// records: no pieces, no masks, every byte read once.  A record boundary x
+// inside chunk k needs the prefix register P_k(x) = raw(chunk[0, x)): the
+// chunk pass stores its team's 32 chain registers (128 B) before every row
+// that holds a boundary (row masks from stream_mark_kernel),
+// stream_points_kernel folds that snapshot with the boundary's row masked
+// to the bytes before x, and stream_finalize_kernel chains chunk registers
+// and prefixes per record [a, E):
+//   s = ~init ^ P(a);  one chunk: s = Z_{E-a}(s) ^ P(E)
+//   else s = Z_{4096-xa}(s) ^ R[k0];  s = Z_4096(s) ^ R[k]  (interior);
+//        s = Z_{xe}(s) ^ P(E);  crc = ~s
+// Bytes of the first and last chunk outside the records (and in the gaps
+// between them) cancel out of every record's value; the whole 4 KiB page of
+// a valid byte is readable.  Boundary points: 2i = start of record i, 2i + 1
+// = its end; an end equal to the next record's start is not computed twice
+// (the finalize reads the start).  Control words (zeroed with the masks by
+// one memset): kStrErr = order violated (every record is then hashed
+// byte-serially by the finalize, so results stay exact), kStrLongs = long
+// records listed.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kStrErr = 0;
+constexpr uint32_t kStrLongs = 1;
+constexpr uint32_t kStrLongChunks = 64;  // more interior chunks: stream_long_kernel
+
+struct StreamGeom
+{
+    uint64_t c_first;  // first chunk index (absolute address / 4096)
+    uint32_t nchunks;
+};
+
+__device__ __forceinline__ StreamGeom stream_geom(const uint8_t* base, const uint64_t* off,
+                                                  uint64_t span)
+{
+    const uint64_t lo = uint64_t(base) + off[0];
+    StreamGeom g;
+    g.c_first = lo / kChunk;
+    g.nchunks = uint32_t((lo + (span ? span : 1) - 1) / kChunk - g.c_first + 1);
+    return g;
+}
+
+// End point 2i + 1 duplicates start point 2i + 2.
+__device__ __forceinline__ bool end_is_next_start(const uint64_t* off, const uint32_t* len,
+                                                  uint64_t count, uint64_t i)
+{
+    return i + 1 < count && off[i + 1] == off[i] + len[i];
+}
+
+// One thread per record: checks the order, marks the rows of the record's
+// start and end in their chunks' row masks.  Row 0 needs no snapshot (the
+// chains are zero there) and chunk starts need no prefix at all, so neither
+// is marked.
+__global__ __launch_bounds__(256) void stream_mark_kernel(const uint8_t* __restrict__ base,
+                                                          const uint64_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ len,
+                                                          uint64_t count, uint64_t span,
+                                                          uint32_t* __restrict__ masks,
+                                                          uint32_t* __restrict__ ctrl)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const StreamGeom g = stream_geom(base, off, span);
+    const uint64_t o = off[i], E = o + len[i];
+    const bool ordered = i + 1 < count ? off[i + 1] >= E && E >= o : E <= off[0] + span && E >= o;
+    if (!ordered) atomicOr(ctrl + kStrErr, 1u);
+    auto mark = [&](uint64_t a) {
+        const uint64_t x = a - g.c_first * kChunk;
+        const uint32_t row = uint32_t(x % kChunk) / kRowBytes;
+        if (row != 0 && x / kChunk < g.nchunks) atomicOr(masks + x / kChunk, 1u << row);
+    };
+    mark(uint64_t(base) + o);
+    if (!end_is_next_start(off, len, count, i)) mark(uint64_t(base) + E);
+}
+
+// The chunk pass: the headline kernel's row ring over chunks k = 0 ..
+// nchunks - 1 of the stream (team t takes chunks t, t + nteams, ...), raw
+// registers (no init) into R[k], and before every marked row the team's
+// chain registers into snaps[(k * 32 + row) * 8 + lane] (16 B per lane).  A
+// wave's 8 teams take 8 consecutive chunks: their masks are read with scalar
+// loads and OR-ed, so a row no team of the wave marks costs two scalar
+// instructions.
+__global__ __launch_bounds__(kBlock, 1) void crc32c_stream_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off, uint64_t span,
+    const uint32_t* __restrict__ masks, uint32_t* __restrict__ R, uint4* __restrict__ snaps,
+    const uint32_t* __restrict__ ctrl, const uint32_t* __restrict__ tables)
+{
+    constexpr int NB = 4, AHEAD = NB - 1, RR = 32;
+    // records out of order: [lo, lo + span) is not known to be readable
+    if (ctrl[kStrErr]) return;
+    stage_tables(tables);
+    const StreamGeom g = stream_geom(base, off, span);
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t li = lane_info();
+    const uint32_t team = (blockIdx.x * kBlock + threadIdx.x) / kTeam;
+    const uint32_t nteams = gridDim.x * kBlock / kTeam;
+    const uint32_t team0 = __builtin_amdgcn_readfirstlane(team & ~7u);  // the wave's first team
+    const uint32_t count = g.nchunks;
+    const uint32_t iters = team0 < count ? (count - team0 + nteams - 1) / nteams : 0;
+    if (iters == 0) return;
+    const uint8_t* c0 = reinterpret_cast<const uint8_t*>(g.c_first * kChunk);
+    auto chunk_of = [&](uint32_t it) {
+        const uint32_t k = team + it * nteams;
+        return k < count ? k : count - 1;
+    };
+    auto wave_mask = [&](uint32_t it) {
+        const uint32_t kb = team0 + it * nteams;  // uniform: scalar loads
+        uint32_t w = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) w |= kb + j < count ? masks[kb + j] : 0u;
+        return w;
+    };
+    auto row_ptr = [&](uint32_t k, int r) { return c0 + uint64_t(k) * kChunk + tl * 16 + r * kRowBytes; };
+
+    uint4 buf[NB];
+    uint32_t k = chunk_of(0);
+    // row masks one chunk ahead (their latency hides behind a chunk's rows)
+    uint32_t wm = wave_mask(0), m = masks[k];
+#pragma unroll
+    for (int r = 0; r < AHEAD; ++r) buf[r] = load16(row_ptr(k, r));
+    for (uint32_t it = 0; it < iters; ++it)
+    {
+        const uint32_t kn = chunk_of(it + 1);
+        const uint32_t wm_next = wave_mask(it + 1), m_next = masks[kn];
+        uint4* snap = snaps + (uint64_t(k) * RR) * kTeam + tl;
+        uint32_t V[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < RR; ++r)
+        {
+            const int ra = r + AHEAD;
+            buf[ra % NB] = load16(ra < RR ? row_ptr(k, ra) : row_ptr(kn, ra - RR));
+            __builtin_amdgcn_sched_barrier(0);
+            if (r != 0 && (wm >> r) & 1u)  // wave-uniform
+            {
+                if ((m >> r) & 1u) snap[r * kTeam] = make_uint4(V[0], V[1], V[2], V[3]);
+            }
+            row_update(V, buf[r % NB], li);
+        }
+        const uint32_t raw = team_fold(V);
+        if (tl == 0 && team + it * nteams < count) R[k] = raw;
+        k = kn;
+        wm = wm_next;
+        m = m_next;
+    }
+}
+
+// One team per boundary point q (record q / 2; its start, or for odd q its
+// end) that is not on a chunk start and not a duplicate: P = raw(chunk[0,
+// x)) from the snapshot of the point's row (zero for row 0) and the row
+// itself, masked to the bytes before x:
+//   W = Z_128(V) ^ masked row;  fold(W) = Z_m(P), m = 128 (row + 1) - x.
+__global__ __launch_bounds__(kBlock, 1) void stream_points_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, uint64_t count, uint64_t span,
+    const uint4* __restrict__ snaps, uint32_t* __restrict__ pval,
+    const uint32_t* __restrict__ ctrl, const uint32_t* __restrict__ tables)
+{
+    if (ctrl[kStrErr]) return;  // out of order: the finalize hashes byte-serially
+    stage_tables(tables);
+    const StreamGeom g = stream_geom(base, off, span);
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t li = lane_info();
+    const uint64_t team = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kTeam;
+    const uint64_t nteams = uint64_t(gridDim.x) * kBlock / kTeam;
+    const uint64_t rel = uint64_t(base) - g.c_first * kChunk;  // chunk-relative = rel + offset
+    // Point q of this team (q = 2i start, 2i + 1 end) -> its inputs, loaded
+    // one point ahead: chunk-relative position, snapshot, row.
+    struct In
+    {
+        uint64_t x;
+        uint4 v, d;
+        bool live;
+    };
+    // the team's points: q = team + j * nteams over [0, 2 count), skipping
+    // ends that repeat the next start or close empty records
+    auto pos_of = [&](uint64_t q, bool* live) {
+        const uint64_t i = q >> 1;
+        const bool is_end = q & 1u;
+        const uint64_t o = off[i];
+        const uint32_t L = len[i];
+        const uint64_t x = rel + o + (is_end ? L : 0u);
+        *live = (x % kChunk) != 0 &&
+                !(is_end && (L == 0 || (i + 1 < count && off[i + 1] == o + L)));
+        return x;
+    };
+    auto fetch = [&](uint64_t q, In& in) {
+        in.x = pos_of(q, &in.live);
+        const uint32_t xc = uint32_t(in.x % kChunk), row = xc / kRowBytes;
+        const uint64_t k = in.x / kChunk;
+        // dead points (an end point may lie one chunk past the stream) read
+        // the zero block and no snapshot
+        const uint8_t* rp = in.live ? reinterpret_cast<const uint8_t*>((g.c_first + k) * kChunk) +
+                                          row * kRowBytes + tl * 16
+                                    : reinterpret_cast<const uint8_t*>(tables + kTabZero);
+        in.d = load16(rp);
+        in.v = in.live && row != 0 ? snaps[(k * 32 + row) * kTeam + tl] : make_uint4(0, 0, 0, 0);
+    };
+    const uint64_t npts = 2 * count;
+    if (team >= npts) return;
+    In cur, nxt;
+    fetch(team, cur);
+    for (uint64_t q = team; q < npts; q += nteams)
+    {
+        const uint64_t qn = q + nteams < npts ? q + nteams : q;
+        fetch(qn, nxt);
+        if (cur.live)  // uniform over the team
+        {
+            const uint32_t xc = uint32_t(cur.x % kChunk);
+            uint32_t V[4] = {cur.v.x, cur.v.y, cur.v.z, cur.v.w};
+            const uint4 d = mask_below(cur.d, int32_t(xc % kRowBytes) - int32_t(tl) * 16);
+            row_update(V, d, li);
+            const uint32_t F = team_fold(V);
+            if (tl == 0)
+            {
+                const uint32_t mneg = kRowBytes - xc % kRowBytes;  // 1 .. 128
+                pval[q] = mneg == kRowBytes ? zglob(tables + kTabZInv128, F)
+                                            : zglob(tables + kTabZNeg + mneg * 1024, F);
+            }
+        }
+        cur = nxt;
+    }
+}
+
+// Z_n, 0 <= n <= 4096, through G^{2^b}, b = 0..12, staged in LDS.
+__device__ __forceinline__ uint32_t zsmall(const uint32_t (*p2)[1024], uint32_t v, uint32_t n)
+{
+#pragma unroll
+    for (int b = 0; b < 13; ++b)
+        if ((n >> b) & 1u) v = zglob(p2[b], v);
+    return v;
+}
+
+// Prefix registers at record i's start and end (chunk-relative a, E).
+__device__ __forceinline__ void record_prefixes(const uint64_t* off, const uint32_t* len,
+                                                uint64_t count, uint64_t i, uint32_t xa,
+                                                uint32_t xe, uint64_t k1, const uint32_t* R,
+                                                const uint32_t* pval, uint32_t* pa, uint32_t* pe)
+{
+    *pa = xa ? pval[2 * i] : 0u;
+    *pe = xe == kChunk ? R[k1] : pval[end_is_next_start(off, len, count, i) ? 2 * i + 2 : 2 * i + 1];
+}
+
+// One thread per record (see the section comment); records with more than
+// kStrLongChunks interior chunks are listed for stream_long_kernel.
+__global__ __launch_bounds__(512) void stream_finalize_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
+    uint64_t span, const uint32_t* __restrict__ R, const uint32_t* __restrict__ pval,
+    uint32_t* __restrict__ ctrl, uint32_t* __restrict__ longs, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables)
+{
+    __shared__ uint32_t p2[13][1024];  // G^{2^b}: Z_1 .. Z_4096
+    __shared__ uint32_t t0[256];
+    for (uint32_t i = threadIdx.x; i < 13 * 1024; i += blockDim.x) p2[i >> 10][i & 1023] = tables[kTabP2 + i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) t0[i] = tables[kTabT + i];
+    __syncthreads();
+    const bool err = ctrl[kStrErr] != 0;
+    const StreamGeom g = stream_geom(base, off, span);
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
+         i += uint64_t(gridDim.x) * blockDim.x)
+    {
+        const uint32_t L = len[i];
+        const uint32_t init = inits ? inits[i] : 0u;
+        if (L == 0)
+        {
+            out[i] = init;
+            continue;
+        }
+        if (err)  // the records are not in order: exact, slowly
+        {
+            const uint8_t* q = base + off[i];
+            uint32_t c = ~init;
+            for (uint32_t j = 0; j < L; ++j) c = t0[(c ^ q[j]) & 0xFFu] ^ (c >> 8);
+            out[i] = ~c;
+            continue;
+        }
+        const uint64_t a = uint64_t(base) + off[i] - g.c_first * kChunk, E = a + L;
+        const uint64_t k0 = a / kChunk, k1 = (E - 1) / kChunk;
+        const uint32_t xa = uint32_t(a % kChunk), xe = uint32_t(E - k1 * kChunk);
+        if (k1 > k0 + 1 + kStrLongChunks)
+        {
+            longs[atomicAdd(ctrl + kStrLongs, 1u)] = uint32_t(i);
+            continue;
+        }
+        uint32_t pa, pe;
+        record_prefixes(off, len, count, i, xa, xe, k1, R, pval, &pa, &pe);
+        uint32_t s = ~init ^ pa;
+        if (k0 == k1)
+            s = zsmall(p2, s, xe - xa) ^ pe;
+        else
+        {
+            s = zsmall(p2, s, kChunk - xa) ^ R[k0];
+            for (uint64_t k = k0 + 1; k < k1; ++k) s = zglob(p2[12], s) ^ R[k];
+            s = zsmall(p2, s, xe) ^ pe;
+        }
+        out[i] = ~s;
+    }
+}
+
+// Records with more than kStrLongChunks interior chunks, one workgroup each:
+// thread t folds interior chunks jj = t + 1024 q (counted from the record's
+// last interior chunk) by Horner with Z_{1024 * 4096}, shifts by Z_{4096 t}
+// and the workgroup XOR-reduces; thread 0 joins the head and the tail.
+__global__ __launch_bounds__(kLongBlock) void stream_long_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
+    uint64_t span, const uint32_t* __restrict__ R, const uint32_t* __restrict__ pval,
+    const uint32_t* __restrict__ ctrl, const uint32_t* __restrict__ longs,
+    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
+    const uint32_t* __restrict__ pow2)
+{
+    __shared__ uint32_t zs[1024];
+    __shared__ uint32_t zc2[10][1024];
+    __shared__ uint32_t red[kLongBlock / 64];
+    if (ctrl[kStrErr]) return;
+    const uint32_t nlong = ctrl[kStrLongs];
+    if (blockIdx.x >= nlong) return;
+    for (uint32_t i = threadIdx.x; i < 1024; i += kLongBlock) zs[i] = tables[kTabZLong + i];
+    for (uint32_t i = threadIdx.x; i < 10 * 1024; i += kLongBlock)
+        zc2[i / 1024][i % 1024] = tables[kTabZC2 + i];
+    __syncthreads();
+    const StreamGeom g = stream_geom(base, off, span);
+    const uint32_t t = threadIdx.x;
+    auto zbig = [&](uint32_t v, uint64_t n) {
+        for (int b = 0; n && b < 48; ++b, n >>= 1)
+            if (n & 1u) v = zglob(pow2 + b * 1024, v);
+        return v;
+    };
+    for (uint32_t q = blockIdx.x; q < nlong; q += gridDim.x)
+    {
+        const uint32_t i = longs[q];
+        const uint32_t L = len[i];
+        const uint64_t a = uint64_t(base) + off[i] - g.c_first * kChunk, E = a + L;
+        const uint64_t k0 = a / kChunk, k1 = (E - 1) / kChunk;
+        const uint64_t nint = k1 - k0 - 1;
+        uint32_t acc = 0;
+        if (t < nint)
+        {
+            const uint64_t n_t = (nint - t + kLongBlock - 1) / kLongBlock;
+            for (uint64_t j = n_t; j-- > 0;) acc = zglob(zs, acc) ^ R[k1 - 1 - (t + j * kLongBlock)];
+            for (int b = 0; b < 10; ++b)
+                if (t & (1u << b)) acc = zglob(zc2[b], acc);
+        }
+        for (int d = 32; d >= 1; d >>= 1) acc ^= __shfl_xor(acc, d);
+        if ((t & 63) == 0) red[t >> 6] = acc;
+        __syncthreads();
+        if (t == 0)
+        {
+            uint32_t c = 0;
+            for (int w = 0; w < kLongBlock / 64; ++w) c ^= red[w];
+            const uint32_t xa = uint32_t(a % kChunk), xe = uint32_t(E - k1 * kChunk);
+            uint32_t pa, pe;
+            record_prefixes(off, len, count, i, xa, xe, k1, R, pval, &pa, &pe);
+            uint32_t h = zbig(~(inits ? inits[i] : 0u) ^ pa, kChunk - xa) ^ R[k0];
+            h = zbig(h, nint * kChunk) ^ c;  // across the interior run
+            out[i] = ~(zbig(h, xe) ^ pe);
+        }
+        __syncthreads();
+    }
+}
+
+uint64_t stream_max_chunks(uint64_t span) { return span / kChunk + 2; }
+
+hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint32_t* inits, uint64_t count, uint64_t span,
+                         const StreamWorkspace& ws, uint32_t* out, const uint32_t* tables,
+                         const uint32_t* pow2, int cus, hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    const uint8_t* b = static_cast<const uint8_t*>(base);
+    const uint64_t maxc = stream_max_chunks(span);
+    hipError_t e = hipMemsetAsync(ws.ctrl, 0, kStreamCtrlWords * 4 + maxc * 4, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(stream_mark_kernel, dim3(uint32_t((count + 255) / 256)), dim3(256), 0,
+                       stream, b, offsets, lengths, count, span, ws.masks, ws.ctrl);
+    const uint64_t need = (maxc + (kBlock / kTeam) - 1) / (kBlock / kTeam);
+    const int grid = int(std::min<uint64_t>(uint64_t(cus), std::max<uint64_t>(need, 1)));
+    hipLaunchKernelGGL(crc32c_stream_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream, b,
+                       offsets, span, ws.masks, ws.R, ws.snaps, ws.ctrl, tables);
+    const uint64_t pneed = (2 * count + (kBlock / kTeam) - 1) / (kBlock / kTeam);
+    const int pgrid = int(std::min<uint64_t>(uint64_t(cus), std::max<uint64_t>(pneed, 1)));
+    hipLaunchKernelGGL(stream_points_kernel, dim3(pgrid), dim3(kBlock), kLdsBytes, stream, b,
+                       offsets, lengths, count, span, ws.snaps, ws.pval, ws.ctrl, tables);
+    const uint64_t fin_blocks = (count + 511) / 512;
+    hipLaunchKernelGGL(stream_finalize_kernel, dim3(uint32_t(fin_blocks < 1024 ? fin_blocks : 1024)),
+                       dim3(512), 0, stream, b, offsets, lengths, inits, count, span, ws.R,
+                       ws.pval, ws.ctrl, ws.longs, out, tables);
+    const uint32_t lgrid = uint32_t(count < 256 ? count : 256);
+    hipLaunchKernelGGL(stream_long_kernel, dim3(lgrid), dim3(kLongBlock), 0, stream, b, offsets,
+                       lengths, inits, count, span, ws.R, ws.pval, ws.ctrl, ws.longs, out, tables,
+                       pow2);
+    return hipGetLastError();
+}
+
 // Allow the 152 KiB dynamic LDS image on the two persistent kernels.
 hipError_t configure_kernels()
 {
@@ -1743,6 +2143,10 @@ hipError_t configure_kernels()
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_direct_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    for (const void* f : {reinterpret_cast<const void*>(&crc32c_stream_kernel),
+                          reinterpret_cast<const void*>(&stream_points_kernel)})
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);

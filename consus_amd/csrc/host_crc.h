@@ -28,5 +28,6 @@ void batch_fixed(const void* base, uint64_t stride, uint64_t length, const uint3
 void note_fallback(int status, uint64_t bytes);
 void note_gpu_call();
 void note_sharded_call();
+void note_stream_batch();
 
 }  // namespace mi_host

@@ -48,6 +48,15 @@ extern "C" {
                                    planned path (plan -> chunks -> finalize), even
                                    for a batch of short records small enough for
                                    the one-launch direct kernel (tests, tuning) */
+#define MI_CRC32C_PACKED 0x10u  /* batches of >= 32 MiB whose records lie in address order
+                                   without overlap (DEVICE: back to back, offsets[i + 1] ==
+                                   offsets[i] + lengths[i], total_bytes their sum): hash
+                                   them as one stream of aligned 4 KiB chunks instead of
+                                   record pieces.  Checked (host: by the engine before
+                                   staging; device: on the device -- if it does not hold,
+                                   every record is hashed byte-serially, exact but slow).
+                                   Opt-in: measured slower than the default piece path on
+                                   BASELINE configs[2]. */
 #define MI_CRC32C_FALLBACK 0x8u /* host memory only: if the GPU engine fails, complete the
                                    call on the engine's CPU path (counted in
                                    mi_crc32c_stats) instead of returning the failure.
@@ -75,6 +84,7 @@ typedef struct mi_crc32c_stats_t
     uint64_t fallback_calls;      /* calls (or shards) completed by the CPU path */
     uint64_t fallback_bytes;      /* bytes the CPU path hashed */
     uint64_t sharded_calls;       /* multi-device calls split over more than one range */
+    uint64_t stream_batches;      /* batches hashed by the stream path (records in order) */
     int32_t last_fallback_status; /* engine status that forced the last fallback (0: none) */
     int32_t reserved;
 } mi_crc32c_stats_t;

@@ -10,8 +10,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import consus_amd as E  # noqa: E402
-if len(sys.argv) > 1:
-    E.LIB_PATH = os.path.abspath(sys.argv[1])
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+PACKED = "--packed" in sys.argv  # MI_CRC32C_PACKED: the stream path
+if args:
+    E.LIB_PATH = os.path.abspath(args[0])
 from consus_amd import workload as W  # noqa: E402
 
 E.init(0)
@@ -23,16 +25,17 @@ d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer
 d_off.upload(off)
 d_len.upload(ln)
 for _ in range(3):
-    E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
+    E.device_batch(data, d_off, d_len, R, out, total_bytes=total, packed=PACKED)
 E.sync()
 times = []
 for _ in range(15):
     E.timer_start()
-    E.device_batch(data, d_off, d_len, R, out, total_bytes=total, asynchronous=True)
+    E.device_batch(data, d_off, d_len, R, out, total_bytes=total, asynchronous=True,
+                   packed=PACKED)
     times.append(E.timer_stop())
 dig = E.crc32c_device(out, R * 4)
 with open(os.path.join(REPO, "tests", "golden", "digests.json")) as f:
     gold = json.load(f)["zipf_seed0x5eed_data0xda7a5eed_1048576"]["digest"]
 ms = float(np.median(times))
-print(f"zipf median {ms:.4f} ms min {min(times):.4f} -> {total / ms / 1e6:.1f} GB/s "
+print(f"{'stream' if PACKED else 'pieces'} zipf median {ms:.4f} ms min {min(times):.4f} -> {total / ms / 1e6:.1f} GB/s "
       f"digest {dig:#010x} {'OK' if dig == gold else 'MISMATCH'}")
