@@ -333,7 +333,6 @@ struct Ctx
 struct ThreadCtx
 {
     Ctx* c[kMaxDevices] = {};
-    int current = -1;  // the device this thread last made current
     ~ThreadCtx()
     {
         for (Ctx*& x : c)
@@ -355,14 +354,17 @@ Ctx* thread_ctx_on(int dev, DeviceState** dout, int* status)
     DeviceState* d = device_state(dev, status);
     if (!d) return nullptr;
     if (dout) *dout = d;
-    if (t_ctx.current != d->ordinal)
+    // The caller (or a library beside us, e.g. torch) may have made another
+    // device current on this thread since our last call: check every time,
+    // allocations follow the current device.
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != d->ordinal)
     {
         if (hipSetDevice(d->ordinal) != hipSuccess)
         {
             *status = fail(MI_CRC32C_EHIP, "hipSetDevice(" + std::to_string(d->ordinal) + ")");
             return nullptr;
         }
-        t_ctx.current = d->ordinal;
     }
     if (Ctx* c = t_ctx.c[d->ordinal]) return c;
     auto* c = new Ctx;
@@ -921,12 +923,10 @@ int mi_crc32c_pipeline_create(size_t max_segment_bytes, size_t max_records, int 
             (st = s.dseg.reserve(max_segment_bytes + 16)) ||
             (st = s.dmeta.reserve(max_records * 16)) || (st = s.ctx.out.reserve(max_records * 4)))
         {
-            t_ctx.current = -1;
             mi_crc32c_pipeline_destroy(p);
             return st;
         }
     }
-    t_ctx.current = -1;  // Ctx::open made the pipeline's device current
     *out = p;
     return MI_CRC32C_OK;
 }
@@ -950,11 +950,8 @@ int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, s
     }
     std::lock_guard<std::mutex> lock(p->mu);
     DeviceState* d = p->dev;
-    if (t_ctx.current != d->ordinal)
-    {
-        HIP_TRY(hipSetDevice(d->ordinal));
-        t_ctx.current = d->ordinal;
-    }
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != d->ordinal) HIP_TRY(hipSetDevice(d->ordinal));
     const uint64_t t = p->next_ticket++;
     auto& s = p->slots[t % p->slots.size()];
     int st;
