@@ -88,8 +88,11 @@ hipError_t launch_direct(const void* base, const uint64_t* offsets, const uint32
                          const uint32_t* tables, const uint32_t* pow2, int grid,
                          hipStream_t stream);
 
+// force_scan: run the separate scan pass even for plans that do not need it
+// (MI_CRC32C_PLAN_SCAN=1, so the tests cover both plan forms).
 hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint32_t* lengths,
-                           uint64_t count, const VarWorkspace& ws, hipStream_t stream);
+                           uint64_t count, const VarWorkspace& ws, hipStream_t stream,
+                           bool force_scan);
 hipError_t launch_var_chunks(const uint32_t* inits, uint64_t count, const VarWorkspace& ws,
                              const uint32_t* tables, int grid, hipStream_t stream);
 hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const uint32_t* lengths,

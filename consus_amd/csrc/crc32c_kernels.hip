@@ -698,21 +698,74 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
     if (threadIdx.x == 0) hdr[kHdrTotal] = carry;
 }
 
-// Each block reads its base in every bin (plan_scan_kernel) and hands its
-// threads their slots.
+// Each block derives its base in every bin from the per-block counts and
+// hands its threads their slots.  Up to kScanFreeBlocks plan blocks (16M
+// records) no scan pass runs: wave b < kBins sums bin b over all blocks and
+// over the blocks before this one (11 x nblocks words, L2-resident), the bin
+// starts are the exclusive scan of the totals, and block 0 publishes the
+// plan header.  Larger plans run plan_scan_kernel first (scanned = true: blk
+// holds the bases).  Interior runs of every length are written here, by the
+// whole wave, 64 items per store; long records (> kLongChunks interior
+// pieces) are also listed for the finalize's block-wide fold.
+constexpr uint32_t kScanFreeBlocks = 4096;
+
 __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, uint64_t count, uint32_t* __restrict__ blk,
     uint32_t nblocks, Item* __restrict__ items, uint64_t item_cap,
     uint32_t* __restrict__ first_pos, uint32_t* __restrict__ int_pos,
-    uint32_t* __restrict__ last_pos, uint32_t* __restrict__ longs)
+    uint32_t* __restrict__ last_pos, uint32_t* __restrict__ longs, bool scanned)
 {
     __shared__ uint32_t bin_base[kBins];
+    __shared__ uint32_t bin_tot[kBins];
     __shared__ uint32_t slot[kBins][kPlanThreads];
     __shared__ uint32_t sh[kPlanThreads / 64][kPacked];
+    __shared__ bool over;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (plan_hdr_d(blk, nblocks)[kHdrTotal] > item_cap) return;  // host re-plans (uniform)
-    if (threadIdx.x < kBins) bin_base[threadIdx.x] = blk[threadIdx.x * nblocks + blockIdx.x];
+    uint32_t* hdr = plan_hdr_d(blk, nblocks);
+    if (scanned)
+    {
+        if (hdr[kHdrTotal] > item_cap) return;  // host re-plans (uniform)
+        if (threadIdx.x < kBins) bin_base[threadIdx.x] = blk[threadIdx.x * nblocks + blockIdx.x];
+    }
+    else
+    {
+        if (wave < kBins)
+        {
+            uint32_t tot = 0, pre = 0;
+            for (uint32_t j = lane; j < nblocks; j += 64)
+            {
+                const uint32_t c = blk[wave * nblocks + j];
+                tot += c;
+                pre += j < blockIdx.x ? c : 0u;
+            }
+            for (int d = 32; d >= 1; d >>= 1)
+            {
+                tot += __shfl_xor(tot, d);
+                pre += __shfl_xor(pre, d);
+            }
+            if (lane == 0)
+            {
+                bin_tot[wave] = tot;
+                bin_base[wave] = pre;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            uint32_t start = 0;
+            for (uint32_t b = 0; b < kBins; ++b)
+            {
+                if (blockIdx.x == 0) hdr[b] = start;
+                bin_base[b] += start;
+                start += bin_tot[b];
+            }
+            if (blockIdx.x == 0) hdr[kHdrTotal] = start;
+            over = start > item_cap;
+        }
+        __syncthreads();
+        if (over) return;  // host re-plans (uniform)
+    }
 
     // this thread's records and their counts (overlaps the loads above)
     const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kPlanPer;
@@ -782,10 +835,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
                 const uint32_t nint = s.n - 2;
                 ip = take(0, nint);
                 int_pos[r] = ip;
-                if (nint > kLongChunks)
-                    longs[atomicAdd(plan_hdr_d(blk, nblocks) + kHdrLongs, 1u)] = uint32_t(r);
-                else
-                    nint_w = nint;
+                if (nint > kLongChunks) longs[atomicAdd(hdr + kHdrLongs, 1u)] = uint32_t(r);
+                nint_w = nint;
                 const uint32_t lp = take(piece_bin(s, s.n - 1), 1);
                 items[lp] = piece_item(s, s.n - 1);
                 last_pos[r] = lp;
@@ -808,38 +859,19 @@ __global__ __launch_bounds__(kPlanThreads) void plan_scatter_kernel(
     }
 }
 
-// Interior pieces of long records, one workgroup per record.
-__global__ __launch_bounds__(kLongBlock) void long_items_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ counters,
-    const uint32_t* __restrict__ longs, const uint32_t* __restrict__ int_pos,
-    Item* __restrict__ items, uint64_t item_cap)
-{
-    if (counters[kHdrTotal] > item_cap) return;
-    const uint32_t nlong = counters[kHdrLongs];
-    for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x)
-    {
-        const uint32_t r = longs[k];
-        const RecShape s = rec_shape(uint64_t(base) + off[r], len[r]);
-        const uint32_t ip = int_pos[r];
-        for (uint32_t i = threadIdx.x; i < s.n - 2; i += kLongBlock)
-            items[ip + i] = interior_item(s.k0, i);
-    }
-}
-
 hipError_t launch_var_plan(const void* base, const uint64_t* offsets, const uint32_t* lengths,
-                           uint64_t count, const VarWorkspace& ws, hipStream_t stream)
+                           uint64_t count, const VarWorkspace& ws, hipStream_t stream,
+                           bool force_scan)
 {
     const uint32_t nb = var_plan_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
     hipLaunchKernelGGL(plan_count_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, count, ws.blk, nb);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, nb);
+    const bool scanned = force_scan || nb > kScanFreeBlocks;
+    if (scanned) hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, ws.blk, nb);
     hipLaunchKernelGGL(plan_scatter_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, count, ws.blk, nb, ws.items, ws.item_cap, ws.first_pos,
-                       ws.int_pos, ws.last_pos, ws.longs);
-    hipLaunchKernelGGL(long_items_kernel, dim3(64), dim3(kLongBlock), 0, stream, b, offsets,
-                       lengths, plan_hdr(ws.blk, nb), ws.longs, ws.int_pos, ws.items, ws.item_cap);
+                       ws.int_pos, ws.last_pos, ws.longs, scanned);
     return hipGetLastError();
 }
 
@@ -1234,13 +1266,15 @@ __device__ __forceinline__ uint32_t last_piece_state(const RecShape& s, const ui
 
 // One thread per record: Horner from ~init over its pieces (see the section
 // comment); records < 32 B byte-serially.
-__global__ __launch_bounds__(512) void crc32c_finalize_kernel(
+constexpr uint32_t kFinBlock = 512;
+__global__ __launch_bounds__(kFinBlock) void crc32c_finalize_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     const uint32_t* __restrict__ partial, const uint32_t* __restrict__ first_pos,
     const uint32_t* __restrict__ int_pos, const uint32_t* __restrict__ last_pos,
     uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
-    const uint32_t* __restrict__ counters, uint64_t item_cap)
+    const uint32_t* __restrict__ counters, uint64_t item_cap,
+    const uint32_t* __restrict__ longs, const uint32_t* __restrict__ pow2)
 {
     // a plan larger than the workspace (an understated total_bytes hint) was
     // not scattered: leave out[] alone rather than read unwritten positions
@@ -1271,7 +1305,7 @@ __global__ __launch_bounds__(512) void crc32c_finalize_kernel(
         }
         else
         {
-            if (s.n >= 2 && s.n - 2 > kLongChunks) continue;  // long_finalize_kernel
+            if (s.n >= 2 && s.n - 2 > kLongChunks) continue;  // the block-wide fold below
             const uint32_t sx = first_seed(s, tables + kTabP2, tables + kTabFInit, inits, r);
             c = first_piece_state(s, p2, zinv, sx, partial[first_pos[r]]);
             if (s.n >= 2)
@@ -1283,50 +1317,33 @@ __global__ __launch_bounds__(512) void crc32c_finalize_kernel(
         }
         out[r] = ~c;
     }
-}
-
-// Long records (> kLongChunks interior pieces): the interior run contributes
-// XOR_jj Z_{C jj}(p[ip + nint - 1 - jj]).  Thread t folds jj = t + 1024 q by
-// Horner with Z_{1024 C}, shifts by Z_{C t} (tables G^{C 2^b}) and the
-// workgroup XOR-reduces; thread 0 adds the first piece carried by
-// Z_{C nint} and the last piece.
-__global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits,
-    const uint32_t* __restrict__ counters, const uint32_t* __restrict__ longs,
-    const uint32_t* __restrict__ partial, const uint32_t* __restrict__ first_pos,
-    const uint32_t* __restrict__ int_pos, const uint32_t* __restrict__ last_pos,
-    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
-    const uint32_t* __restrict__ pow2, uint64_t item_cap)
-{
-    __shared__ uint32_t zs[1024];
-    __shared__ uint32_t zc2[10][1024];
-    __shared__ uint32_t red[kLongBlock / 64];
-    if (counters[kHdrTotal] > item_cap) return;
+    // Long records (listed by plan_scatter_kernel), one workgroup each:
+    // their interior run contributes XOR_jj Z_{C jj}(p[ip + nint - 1 - jj]).
+    // Thread t folds jj = t + 512 q by Horner with Z_{512 C}, shifts by
+    // Z_{C t} (G^{C 2^b}, b < 9) and the workgroup XOR-reduces; thread 0 adds
+    // the first piece carried by Z_{C nint} and the last piece.  Their tables
+    // are read from global memory (L2): long records are rare.
     const uint32_t nlong = counters[kHdrLongs];
     if (blockIdx.x >= nlong) return;
-    for (uint32_t i = threadIdx.x; i < 1024; i += kLongBlock) zs[i] = tables[kTabZLong + i];
-    for (uint32_t i = threadIdx.x; i < 10 * 1024; i += kLongBlock)
-        zc2[i / 1024][i % 1024] = tables[kTabZC2 + i];
-    __syncthreads();
+    static_assert(kFinBlock == 512, "long fold stride: Z_{512 C} = G^{C 2^9}");
+    __shared__ uint32_t red[kFinBlock / 64];
     const uint32_t t = threadIdx.x;
-    const uint32_t* p2 = tables + kTabP2;
-    const uint32_t* zinv = tables + kTabZInv128;
+    const uint32_t* zs = tables + kTabZC2 + 9 * 1024;
     for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x)
     {
         const uint32_t r = longs[k];
-        const uint8_t* p = base + off[r];
-        const RecShape s = rec_shape(uint64_t(p), len[r]);
+        const RecShape s = rec_shape(uint64_t(base) + off[r], len[r]);
         const uint32_t nint = s.n - 2;
         const uint32_t ip = int_pos[r];
         uint32_t acc = 0;
         if (t < nint)
         {
-            const uint32_t n_t = (nint - t + kLongBlock - 1) / kLongBlock;
+            const uint32_t n_t = (nint - t + kFinBlock - 1) / kFinBlock;
             for (uint32_t q = n_t; q-- > 0;)
-                acc = zglob(zs, acc) ^ partial[ip + nint - 1 - (t + q * kLongBlock)];
-            for (int b = 0; b < 10; ++b)
-                if (t & (1u << b)) acc = zglob(zc2[b], acc);
+                acc = zglob(zs, acc) ^ partial[ip + nint - 1 - (t + q * kFinBlock)];
+#pragma unroll 1
+            for (int b = 0; b < 9; ++b)
+                if (t & (1u << b)) acc = zglob(tables + kTabZC2 + b * 1024, acc);
         }
         for (int d = 32; d >= 1; d >>= 1) acc ^= __shfl_xor(acc, d);
         if ((t & 63) == 0) red[t >> 6] = acc;
@@ -1334,10 +1351,11 @@ __global__ __launch_bounds__(kLongBlock) void long_finalize_kernel(
         if (t == 0)
         {
             uint32_t c = 0;
-            for (int w = 0; w < kLongBlock / 64; ++w) c ^= red[w];
-            uint32_t h = first_piece_state(s, p2, zinv, first_seed(s, p2, tables + kTabFInit, inits, r),
+            for (int w = 0; w < kFinBlock / 64; ++w) c ^= red[w];
+            uint32_t h = first_piece_state(s, p2, zinv, first_seed(s, tables + kTabP2, tables + kTabFInit, inits, r),
                                            partial[first_pos[r]]);
             uint64_t n = uint64_t(nint) * kChunk;  // bytes of the interior run
+#pragma unroll 1
             for (int b = 0; n && b < 48; ++b, n >>= 1)
                 if (n & 1u) h = zglob(pow2 + b * 1024, h);
             c ^= h;
@@ -1355,16 +1373,12 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
     if (count == 0) return hipSuccess;
     const uint8_t* b = static_cast<const uint8_t*>(base);
     // four 512-thread workgroups per CU fit the 37 KB of tables each stages
-    const uint64_t fin_blocks = (count + 511) / 512;
+    const uint64_t fin_blocks = (count + kFinBlock - 1) / kFinBlock;
     hipLaunchKernelGGL(crc32c_finalize_kernel, dim3(uint32_t(fin_blocks < 1024 ? fin_blocks : 1024)),
-                       dim3(512), 0,
+                       dim3(kFinBlock), 0,
                        stream, b, offsets, lengths, inits, count, ws.partial, ws.first_pos,
                        ws.int_pos, ws.last_pos, out, tables,
-                       plan_hdr(ws.blk, var_plan_blocks(count)), ws.item_cap);
-    const uint32_t grid = uint32_t(count < 256 ? count : 256);
-    hipLaunchKernelGGL(long_finalize_kernel, dim3(grid), dim3(kLongBlock), 0, stream, b, offsets,
-                       lengths, inits, plan_hdr(ws.blk, var_plan_blocks(count)), ws.longs, ws.partial,
-                       ws.first_pos, ws.int_pos, ws.last_pos, out, tables, pow2, ws.item_cap);
+                       plan_hdr(ws.blk, var_plan_blocks(count)), ws.item_cap, ws.longs, pow2);
     return hipGetLastError();
 }
 

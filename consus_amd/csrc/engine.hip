@@ -428,6 +428,17 @@ int run_stream(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     return MI_CRC32C_OK;
 }
 
+// MI_CRC32C_PLAN_SCAN=1: plans always take the separate scan pass (which
+// only plans of more than 16M records need), so tests exercise both forms.
+bool plan_scan_forced()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("MI_CRC32C_PLAN_SCAN");
+        return e && !std::strcmp(e, "1");
+    }();
+    return v;
+}
+
 // ---- the variable-length pipeline on device-resident arrays -------------
 // All pointers device pointers; enqueued on c->stream.  `total_bytes` bounds
 // the plan size (0 = unknown -> one read-back).  `span` > 0: the records are
@@ -474,7 +485,7 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
                         c->partial.as<uint32_t>(),   c->first_pos.as<uint32_t>(),
                         c->int_pos.as<uint32_t>(),   c->last_pos.as<uint32_t>(),
                         c->longs.as<uint32_t>(),     cap};
-        HIP_TRY(launch_var_plan(base, off, len, count, ws, c->stream));
+        HIP_TRY(launch_var_plan(base, off, len, count, ws, c->stream, plan_scan_forced()));
         if (!total_bytes)
         {
             uint32_t* h = c->pin_small.as<uint32_t>();

@@ -197,26 +197,31 @@ def test_rccl_single_rank_allgather(engine, oracle):
         engine.comm_destroy()
 
 
-def test_var_many_records_multi_tile_plan(engine, oracle):
-    """6.5M short records: > 1,587 plan blocks, so the bin scan runs over
-    several LDS tiles, and the scatter's per-block bases come from it."""
-    rng = np.random.default_rng(21)
-    count = 6_500_000
-    lengths = rng.integers(0, 97, count, dtype=np.uint32)
-    lengths[rng.integers(0, count, 64)] = 70_000            # a few multi-chunk records
-    offsets = np.zeros(count, dtype=np.uint64)
-    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
-    total = int(lengths.sum(dtype=np.uint64))
-    data = engine.DeviceBuffer(total + 16)
-    data.fill_splitmix64(0x5CA1E)
-    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
-                           engine.DeviceBuffer(count * 4))
-    d_off.upload(offsets)
-    d_len.upload(lengths)
-    engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=total)
-    got = d_out.download(np.uint32, count)
-    host = data.download(np.uint8, total)
-    assert np.array_equal(got, oracle.batch(host, offsets, lengths))
+def test_var_many_records_plan(engine, oracle):
+    """6.5M short records (1,587 plan blocks): the scatter derives its bin
+    bases from the per-block counts, no scan pass."""
+    from tests import _plan_forms
+    _plan_forms.many_records(engine, oracle)
+
+
+def test_var_long_records_block_fold(engine, oracle):
+    """Records with 65 - 770 interior pieces: interior items written by the
+    scatter's wave loop, the interior run folded block-wide by the finalize."""
+    from tests import _plan_forms
+    _plan_forms.long_records(engine, oracle)
+
+
+def test_var_plan_scan_pass_forced():
+    """The same two batches with the separate scan pass that plans of more
+    than 16M records take (MI_CRC32C_PLAN_SCAN=1, one child process)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MI_CRC32C_PLAN_SCAN="1")
+    r = subprocess.run([sys.executable, os.path.join(here, "_plan_forms.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "plan forms ok 1" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 
 @PATHS
