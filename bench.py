@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--sustain-seconds", type=float, default=3.0,
+                    help="fixed4k: after the timed region, launch back to back for this long and "
+                         "report the sustained per-GPU rate (clock/power droop check; 0 = off)")
     ap.add_argument("--config", default="fixed4k",
                     choices=["fixed4k", "zipf", "stream", "pcie4k", "single", "dlog"],
                     help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2] "
@@ -742,6 +745,27 @@ def main():
         want = [combine_digests(exp[i * k:(i + 1) * k], [blk] * k) for i in range(world)]
         verified = all(digests[i] == want[i] for i in range(world))
 
+    # Sustained rate, outside the timed region: back-to-back launches for a
+    # few seconds (the per-launch rate must not droop with clocks or power;
+    # it also keeps the GPU busy long enough for a utilisation sampler).
+    sustained = None
+    if args.sustain_seconds > 0:
+        E.sync()
+        E.timer_start()
+        n_s, t_s = 0, time.perf_counter()
+        while time.perf_counter() - t_s < args.sustain_seconds:
+            for _ in range(100):
+                E.device_batch_fixed(data, L, L, R, out, asynchronous=True)
+            n_s += 100
+            E.sync()
+        s_ms = E.timer_stop()
+        s_gbs = n_s * R * L / (s_ms * 1e-3) / 1e9
+        sustained = {"launches": n_s, "seconds": round(s_ms * 1e-3, 3),
+                     "launch_ms": round(s_ms / n_s, 4), "achieved_gb_s": round(s_gbs, 1),
+                     "frac": round(s_gbs / HBM_PEAK_GBS, 4)}
+        if crcs_dev_digest != E.crc32c_device(out, R * 4):
+            sustained["error"] = "CRC vector changed under sustained launches"
+
     total_bytes = world * R * L * args.steps
     value = total_bytes / wall / 2**30
     # per-GPU kernel rate; at N > 1 from the slowest rank's launches
@@ -779,6 +803,7 @@ def main():
         },
         "digest_verified": verified,
         "digests": [f"{d:#010x}" for d in digests],
+        "sustained": sustained,
     }
     if world == 1 and not args.no_cpu:
         rec["cpu_baseline"] = cpu_baseline(args)

@@ -141,6 +141,32 @@ def test_pipeline_segments_pageable_and_pinned(engine, oracle, max_entry):
     pinned.free()
 
 
+def test_pipeline_pageable_reuse_after_submit(engine, oracle):
+    """The ownership contract of include/consus_crc32c.h: submit() copies a
+    pageable segment and the offsets/lengths before it returns, so the caller
+    may overwrite all three at once (one buffer refilled for every segment, as
+    a log writer does); the CRCs are of the bytes at submit time."""
+    rng = np.random.default_rng(81)
+    p = engine.Pipeline(4 << 20, 16384, depth=3)
+    segs = [make_frames(rng, 2 << 20, 3000) for _ in range(6)]
+    work = np.zeros(2 << 20, dtype=np.uint8)
+    outs, tickets = [], []
+    for buf, off, ln in segs:
+        work[:buf.size] = buf
+        w_off, w_len = off.copy(), ln.copy()
+        out = np.zeros(off.size, dtype=np.uint32)
+        tickets.append(p.submit(work[:buf.size], w_off, w_len, out))
+        work[:] = rng.integers(0, 256, work.size, dtype=np.uint8)  # refilled at once
+        w_off[:] = 0
+        w_len[:] = 1
+        outs.append(out)
+    for t in tickets:
+        p.wait(t)
+    for (buf, off, ln), out in zip(segs, outs):
+        assert np.array_equal(out, oracle.batch(buf, off, ln))
+    p.close()
+
+
 def test_device_batch_var_and_combine(engine, oracle):
     rng = np.random.default_rng(12)
     count = 20000
