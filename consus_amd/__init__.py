@@ -112,7 +112,8 @@ class Stats(C.Structure):
                 ("fallback_bytes", C.c_uint64), ("sharded_calls", C.c_uint64),
                 ("stream_batches", C.c_uint64),
                 ("last_fallback_status", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("reserved", C.c_int32),
+                ("sorted_batches", C.c_uint64)]
 
 _lib = None
 

@@ -105,6 +105,25 @@ constexpr uint32_t kPlanHdrTotal = kBins;
 constexpr uint32_t kPlanHdrWords = kBins + 4;
 inline uint32_t* plan_hdr(uint32_t* blk, uint32_t nblocks) { return blk + kBins * nblocks; }
 
+// Sorted path (launch_sorted): whole records per team, binned by row count
+// inside each workgroup's cost-balanced share; two launches, no plan/finalize.
+struct SortedWorkspace
+{
+    uint64_t* blk_cost;  // sorted_blocks(count)
+    uint32_t* ctrl;      // 4 words: item cursor, overflow flag
+    uint4* items;        // item_cap 16-B descriptors
+    uint64_t item_cap;   // sorted_item_cap(count, total_bytes)
+};
+// batches of at least this many bytes (the total known) take the sorted path
+constexpr uint64_t kSortedMinBytes = 64ull << 20;
+constexpr uint64_t kSortedMaxCount = 1ull << 30;
+uint32_t sorted_blocks(uint64_t count);
+uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes);
+hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint32_t* inits, uint64_t count, const SortedWorkspace& ws,
+                         uint32_t* out, const uint32_t* tables, const uint32_t* pow2, int grid,
+                         hipStream_t stream);
+
 // Batches of records in address order hashed as one stream of aligned 4 KiB
 // chunks over [base + offsets[0], + span) (launch_stream).
 constexpr uint32_t kStreamCtrlWords = 16;

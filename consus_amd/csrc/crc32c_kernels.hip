@@ -2168,6 +2168,642 @@ hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Variable-length batches, sorted path: one team per
+// whole record, records binned by row count inside each workgroup's share.
+//   sorted_cost_kernel:   per block of 4,096 records, the sum of the records'
+//       costs (rows plus a fold allowance per item).  Records shorter than
+//       4 B are finished here byte-serially; split records get out[r] = ~0.
+//   crc32c_sorted_kernel: with C the total cost and G workgroups, workgroup b
+//       takes the items whose cost starts in [C b / G, C (b + 1) / G), a
+//       contiguous run of records.  It bins them by row count in LDS (largest
+//       first), writes 16-B descriptors to the workspace, and its 16 waves
+//       take groups of 8 items (one per team) from an LDS counter, largest
+//       first (LPT).  A team hashes its item's 128-B rows right-aligned to the
+//       group's row count (padded to the ring's 4 rows) through the headline
+//       kernel's row ring: ~init is XORed into the record's first 4 bytes
+//       (identity 3), bytes outside the item are masked, rows before it are
+//       read from a zero block, and crc = ~Z_{-m}(fold), m = ceil128(E) - E.
+//   Records longer than 64 KiB are cut into 64 KiB pieces from their start;
+//   each piece XORs Z_{E - pe}(raw(piece)) into out[r] (identity 1).
+// No plan/finalize passes over the items: one small launch, then the hash.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
+constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 1;  // rows of the largest item (513)
+constexpr uint32_t kSortBins = kSortRows;                         // bin = kSortRows - rows
+constexpr uint32_t kSortFold = 2;            // cost allowance per item, in rows (fold, masks)
+constexpr uint32_t kSortPer = 1;             // records per thread of a cost block
+constexpr uint32_t kSortRecs = kPlanThreads * kSortPer;
+constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a split record
+constexpr uint32_t kSortFirst = 0x40000000u;  // ... its first piece (carries the init)
+constexpr uint32_t kSortRecMask = 0x3FFFFFFFu;
+constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
+
+// measurement builds only (tools/build_variant.sh), results are wrong: stop
+// after the binning (1), the block search (2), the boundaries (3), the
+// table staging (4): times the prologue's phases
+#ifndef MI_SORT_STOP
+#define MI_SORT_STOP 0
+#endif
+
+uint32_t sorted_blocks(uint64_t count) { return uint32_t((count + kSortRecs - 1) / kSortRecs); }
+
+struct SortCost
+{
+    uint64_t cost;       // all the record's items
+    uint32_t n;          // items (pieces); 0: finished by sorted_cost_kernel (L < 4)
+    uint32_t c_int;      // cost of every piece but the last
+    uint32_t rows_full;  // rows of every piece but the last
+    uint32_t rows_last;
+};
+
+__device__ __forceinline__ SortCost sort_cost(uint64_t a, uint32_t L)
+{
+    SortCost s{0, 0, 0, 0, 0};
+    if (L < 4) return s;
+    s.n = uint32_t((uint64_t(L) + kSortPiece - 1) / kSortPiece);
+    s.rows_full = uint32_t(kSortPiece / kRowBytes) + ((a & (kRowBytes - 1)) ? 1u : 0u);
+    const uint64_t ps = a + uint64_t(s.n - 1) * kSortPiece, E = a + L;
+    s.rows_last = uint32_t(((E + kRowBytes - 1) >> 7) - (ps >> 7));
+    s.c_int = s.rows_full + kSortFold;
+    s.cost = uint64_t(s.n - 1) * s.c_int + s.rows_last + kSortFold;
+    return s;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), l));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l));
+    return uint64_t(lo) | (uint64_t(hi) << 32);
+}
+
+__global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
+    uint64_t* __restrict__ blk_cost, uint32_t* __restrict__ ctrl, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables)
+{
+    __shared__ uint64_t sh[kPlanThreads / 64];
+    const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kSortPer;
+    uint64_t c = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kSortPer; ++q)
+    {
+        const uint64_t r = r0 + q;
+        if (r >= count) break;
+        const uint8_t* p = base + off[r];
+        const uint32_t L = len[r];
+        if (L < 4)
+        {
+            uint32_t x = ~(inits ? inits[r] : 0u);
+            for (uint32_t i = 0; i < L; ++i) x = tables[kTabT + ((x ^ p[i]) & 0xFFu)] ^ (x >> 8);
+            out[r] = ~x;
+            continue;
+        }
+        const SortCost s = sort_cost(uint64_t(p), L);
+        c += s.cost;
+        if (s.n > 1) out[r] = ~0u;  // the pieces XOR their parts in
+    }
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+    if ((threadIdx.x & 63u) == 0) sh[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        uint64_t t = 0;
+        for (uint32_t w = 0; w < kPlanThreads / 64; ++w) t += sh[w];
+        blk_cost[blockIdx.x] = t;
+        if (blockIdx.x == 0)
+        {
+            ctrl[0] = 0;  // item allocation cursor
+            ctrl[1] = 0;  // overflow flag
+        }
+    }
+}
+
+// LDS of the sorted kernel beyond the table image.
+struct SortShared
+{
+    uint32_t bins[kSortBins];  // item counts per bin, then their cursors
+    uint32_t n_items;
+    uint32_t item_base;
+    uint32_t next_group;
+    uint32_t bound[4];         // (record, piece) of the first item and of the end
+    uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
+    uint64_t pre[2];           // cost before those blocks
+    uint64_t target[2];
+    uint64_t wsum[kBlock / 64];
+};
+constexpr uint32_t kLdsSorted = kLdsBytes + uint32_t((sizeof(SortShared) + 255) & ~size_t(255));
+static_assert(kLdsSorted <= 163840, "sorted kernel LDS");
+static_assert(kSortRecs == 2 * 512, "sort_resolve: 512 threads x 2 records per cost block");
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        const uint64_t y = __shfl_up(x, d);
+        if (lane >= uint32_t(d)) x += y;
+    }
+    return x;
+}
+
+// Exclusive prefix of v over the 1024-thread workgroup, and the total.
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* wsum, uint64_t& total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t x = wave_incl_scan64(v);
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (uint32_t w = 0; w < kBlock / 64; ++w)
+    {
+        const uint64_t s = wsum[w];
+        pre += w < wave ? s : 0;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+// Wave 0: the total cost C, the targets C b / G and C (b + 1) / G, and the
+// cost blocks holding them (each lane takes 16 consecutive blocks per round,
+// so 1,024 blocks cost one round trip).
+__device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ blk_cost, uint32_t nb,
+                                                 uint64_t count, SortShared& S)
+{
+    constexpr uint32_t K = 16;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t tot = 0;
+    for (uint32_t c0 = 0; c0 < nb; c0 += 64 * K)
+    {
+        uint64_t v[K];
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k)
+        {
+            const uint32_t j = c0 + lane * K + k;
+            v[k] = j < nb ? blk_cost[j] : 0;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) tot += v[k];
+    }
+    for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d);
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    uint64_t T[2];
+    T[0] = tot / G * b + (tot % G) * b / G;
+    T[1] = b + 1 == G ? tot : tot / G * (b + 1) + (tot % G) * (b + 1) / G;
+    if (lane == 0)
+        for (int h = 0; h < 2; ++h)
+        {
+            S.blk[h] = nb;  // past the end unless found
+            S.pre[h] = 0;
+            S.target[h] = T[h];
+            S.bound[2 * h] = uint32_t(count);
+            S.bound[2 * h + 1] = 0;
+        }
+    bool found[2] = {false, false};
+    uint64_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nb && !(found[0] && found[1]); c0 += 64 * K)
+    {
+        uint64_t v[K], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k)
+        {
+            const uint32_t j = c0 + lane * K + k;
+            v[k] = j < nb ? blk_cost[j] : 0;
+            sum += v[k];
+        }
+        const uint64_t incl = carry + wave_incl_scan64(sum), excl = incl - sum;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+        {
+            const bool mine = !found[h] && excl <= T[h] && T[h] < incl;
+            if (mine)
+            {
+                uint64_t p = excl;
+                uint32_t k = 0;
+                while (p + v[k] <= T[h]) p += v[k++];  // stops inside this lane's run
+                S.blk[h] = c0 + lane * K + k;
+                S.pre[h] = p;
+            }
+            found[h] = found[h] || __builtin_amdgcn_ballot_w64(mine) != 0;
+        }
+        carry = readlane64(incl, 63);
+    }
+}
+
+// The first item (record, piece) whose cost starts at or after each target:
+// threads 512 h .. 512 h + 511 resolve target h inside its cost block (two
+// records per thread), both at once.  Result in bound[2 h], bound[2 h + 1].
+__device__ __forceinline__ void sort_resolve(const uint8_t* base, const uint64_t* off,
+                                             const uint32_t* len, uint64_t count, uint32_t nb,
+                                             SortShared& S)
+{
+    const uint32_t h = threadIdx.x >> 9, t = threadIdx.x & 511u;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t j = S.blk[h];
+    const uint64_t r0 = uint64_t(j) * kSortRecs + 2 * t;
+    SortCost sc[2];
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q)
+    {
+        sc[q] = SortCost{0, 0, 0, 0, 0};
+        if (j < nb && r0 + q < count) sc[q] = sort_cost(uint64_t(base) + off[r0 + q], len[r0 + q]);
+        mine += sc[q].cost;
+    }
+    const uint64_t x = wave_incl_scan64(mine);
+    if (lane == 63) S.wsum[wave] = x;
+    __syncthreads();
+    uint64_t start = x - mine;
+    for (uint32_t w = 8 * h; w < wave; ++w) start += S.wsum[w];
+    const uint64_t tl = S.target[h] - S.pre[h];
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q)
+    {
+        if (sc[q].cost && start <= tl && tl < start + sc[q].cost)
+        {
+            const uint64_t i = (tl - start + sc[q].c_int - 1) / sc[q].c_int;  // first piece at/after
+            S.bound[2 * h] = uint32_t(i < sc[q].n ? r0 + q : r0 + q + 1);
+            S.bound[2 * h + 1] = uint32_t(i < sc[q].n ? i : 0);
+        }
+        start += sc[q].cost;
+    }
+    __syncthreads();
+}
+
+// Lanes of the wave (among `active` ones) with the same 10-bit key: one
+// ballot per key bit (no contended LDS atomics when most keys repeat).
+__device__ __forceinline__ uint64_t match_key10(uint32_t key, bool active)
+{
+    uint64_t eq = __builtin_amdgcn_ballot_w64(active);
+#pragma unroll
+    for (int b = 0; b < 10; ++b)
+    {
+        const bool bit = (key >> b) & 1u;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(bit);
+        eq &= bit ? m : ~m;
+    }
+    return eq;
+}
+
+// A team's view of its item within the group window [w1 - 128 n, w1) of n rows.
+struct SortView
+{
+    uint64_t p0;     // this lane's 16 B in window row 0
+    int32_t f;       // the item's first row (n - rows)
+    int32_t lo, hi;  // rows in which this lane reads item bytes (lo > hi: none)
+    uint4 kf;        // row f: keep masks (bytes from the item start on)
+    uint4 xf;        // row f: ~init over the record's first 4 bytes (0: none)
+    uint32_t xs;     // row f + 1, dword 0: the init word's spill (0: none)
+    uint4 ke;        // row n - 1: keep masks (bytes before the item end)
+    uint32_t m;      // bytes masked after the item in the last row
+    uint32_t recf;   // record | flags, kSortNone: no item
+};
+
+__device__ __forceinline__ uint32_t sort_rows(const uint4& d)
+{
+    const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
+    return d.z ? uint32_t(((ps + d.z + kRowBytes - 1) >> 7) - (ps >> 7)) : 0u;
+}
+
+// ~init placed at byte offset q of a 16-B block (q in -3..15), dword k.
+__device__ __forceinline__ uint32_t init_dword(uint32_t ninit, int32_t q, int k)
+{
+    const int32_t dd = 4 * k - q;  // init byte 0 sits dd bytes before this dword
+    const uint32_t s = uint32_t(min(max(32 + 8 * dd, 0), 63));
+    const uint32_t x = uint32_t((uint64_t(ninit) << 32) >> s);
+    return (dd > -4 && dd < 4) ? x : 0u;
+}
+
+// The masks depend on the record's init, loaded here and consumed a group
+// later (sort_view runs for the NEXT group), so the load costs no wait.
+__device__ __forceinline__ SortView sort_view(const uint4& d, int32_t n, uint32_t tl,
+                                              const uint32_t* __restrict__ inits,
+                                              const uint32_t* __restrict__ zero_word,
+                                              const uint32_t* __restrict__ ones_word)
+{
+    SortView v;
+    const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
+    const uint64_t E = ps + d.z;
+    const uint64_t w0 = ps & ~uint64_t(kRowBytes - 1), w1 = (E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
+    const int32_t rows = int32_t(sort_rows(d));
+    v.recf = d.z ? d.w : kSortNone;
+    v.f = n - rows;
+    v.p0 = w1 - uint64_t(n) * kRowBytes + tl * 16u;
+    const int32_t s0 = int32_t(ps - w0);
+    const int32_t bs = min(max(s0 - int32_t(tl) * 16, 0), 16);
+    v.lo = v.f + (bs >= 16 ? 1 : 0);
+    const int32_t ce = min(max(int32_t(E - (w1 - kRowBytes)) - int32_t(tl) * 16, 0), 16);
+    v.hi = n - 1 - (ce == 0 ? 1 : 0);
+    if (!d.z)
+    {
+        v.lo = n;
+        v.hi = -1;
+    }
+    v.m = uint32_t(w1 - E);
+    v.kf = make_uint4(keep_from(bs, 0), keep_from(bs, 1), keep_from(bs, 2), keep_from(bs, 3));
+    v.ke = make_uint4(keep_below(ce, 0), keep_below(ce, 1), keep_below(ce, 2), keep_below(ce, 3));
+    const bool with_init = d.z && (!(d.w & kSortMulti) || (d.w & kSortFirst));
+    // always one load (0 without inits, all ones where no init word goes in)
+    const uint32_t ninit = ~*(!with_init ? ones_word : inits ? inits + (d.w & kSortRecMask) : zero_word);
+    const int32_t q = s0 - int32_t(tl) * 16;  // the record's first byte in this lane's block of row f
+    v.xf = make_uint4(init_dword(ninit, q, 0), init_dword(ninit, q, 1), init_dword(ninit, q, 2),
+                      init_dword(ninit, q, 3));
+    v.xs = init_dword(ninit, q - int32_t(kRowBytes), 0);  // lane 0 of row f + 1, when s0 > 124
+    return v;
+}
+
+__device__ __forceinline__ uint32_t zshift48(const uint32_t* __restrict__ pow2, uint32_t v, uint64_t n)
+{
+    for (int k = 0; n && k < 48; ++k, n >>= 1)
+        if (n & 1u) v = zglob(pow2 + k * 1024, v);
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
+    const uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
+    uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ out,
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2)
+{
+    SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = 0;
+    if (threadIdx.x == 0) S.next_group = 0;
+    stage_tables(tables);  // ends with a barrier
+    if (MI_SORT_STOP == 4) return;
+
+    // (1) Wave 0: the two targets and the cost blocks holding them.
+    if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
+    __syncthreads();
+    if (MI_SORT_STOP == 2) return;
+    // (2) Exact (record, piece) boundaries of this workgroup's items.
+    sort_resolve(base, off, len, count, nb, S);
+    if (MI_SORT_STOP == 3) return;
+
+    // (3) Bin the items by row count (pass 1), place the bins largest first,
+    // write the descriptors (pass 2).  Whole records and last pieces take one
+    // LDS atomic per distinct row count of a wave (match_key10); the full
+    // pieces of split records one per record.
+    const uint32_t rlo = S.bound[0], klo0 = S.bound[1], rhi = S.bound[2], khi0 = S.bound[3];
+    const uint64_t rend = min(uint64_t(rhi) + (khi0 ? 1u : 0u), count);
+    auto bin_pass = [&](uint4* my_items) {
+        for (uint64_t r = uint64_t(rlo) + threadIdx.x; r < rend; r += kBlock)
+        {
+            const uint64_t a = uint64_t(base) + off[r];
+            const uint32_t L = len[r];
+            const SortCost s = sort_cost(a, L);
+            const uint32_t klo = r == rlo ? klo0 : 0u;
+            const uint32_t khi = r == rhi ? khi0 : s.n;
+            const uint32_t lim = s.n ? s.n - 1 : 0u;  // pieces before the last
+            const uint32_t nf = min(khi, lim) > klo ? min(khi, lim) - klo : 0u;
+            const bool last = s.n != 0 && klo < khi && khi == s.n;
+            const uint32_t flags = s.n > 1 ? kSortMulti : 0u;
+            auto desc = [&](uint32_t k) {
+                const uint64_t ps = a + uint64_t(k) * kSortPiece;
+                const uint32_t pl = uint32_t(min<uint64_t>(kSortPiece, a + L - ps));
+                return make_uint4(uint32_t(ps), uint32_t(ps >> 32), pl,
+                                  uint32_t(r) | flags | (k == 0 ? kSortFirst : 0u));
+            };
+            if (nf)
+            {
+                const uint32_t p = atomicAdd(&S.bins[kSortRows - s.rows_full], nf);
+                if (my_items)
+                    for (uint32_t i = 0; i < nf; ++i) my_items[p + i] = desc(klo + i);
+            }
+            const uint32_t key = kSortRows - s.rows_last;
+            const uint64_t eq = match_key10(key, last);
+            const uint32_t rank = uint32_t(__builtin_popcountll(eq & ((uint64_t(1) << lane) - 1)));
+            uint32_t pos = 0;
+            if (last && rank == 0) pos = atomicAdd(&S.bins[key], uint32_t(__builtin_popcountll(eq)));
+            if (my_items)
+            {
+                pos = uint32_t(__shfl(int(pos), last ? int(__builtin_ctzll(eq)) : int(lane)));
+                if (last) my_items[pos + rank] = desc(s.n - 1);
+            }
+        }
+    };
+    bin_pass(nullptr);
+    __syncthreads();
+    {
+        const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
+        uint64_t total;
+        const uint32_t e = uint32_t(block_excl_scan64(c, S.wsum, total));
+        if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = e;
+        if (threadIdx.x == 0)
+        {
+            S.n_items = uint32_t(total);
+            uint32_t b = __hip_atomic_fetch_add(ctrl, uint32_t(total), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+            if (uint64_t(b) + total > item_cap)
+            {
+                ctrl[1] = 1;  // workspace too small (understated total_bytes): out[] left alone
+                S.n_items = 0;
+            }
+            S.item_base = b;
+        }
+    }
+    __syncthreads();
+    uint4* const my_items = items + S.item_base;
+    const uint32_t n_items = S.n_items;
+    if (n_items) bin_pass(my_items);
+    __syncthreads();
+    if (n_items == 0 || MI_SORT_STOP == 1) return;
+
+    // (4) Groups of 8 items, largest first, one LDS grab per group.
+    const uint32_t n_groups = (n_items + 7) / 8;
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t tw = lane / kTeam;
+    const uint32_t li = lane_info();
+    const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
+    const uint32_t* zero_word = tables + kTabZero;
+    const uint32_t* ones_word = tables + kTabFInit;  // Z_0(~0) = 0xFFFFFFFF
+    const uint32_t* zneg = tables + kTabZNeg;
+    // An item is finished one group late: right after its fold, lane q < 4 of
+    // the team looks up byte q of the fold in the Z_{-m} table (one load per
+    // lane, issued with no wait); the next group's finish XORs the four
+    // entries and stores.  (Finishing at once drained the row ring.)
+    uint32_t pz = 0;               // this lane's Z_{-m} entry of the pending item
+    uint32_t p_recf = kSortNone;   // the pending item's record | flags
+    uint64_t p_pe = 0;             // its end (lane 0; split records only)
+    auto flush = [&]() {
+        uint32_t v = pz;
+        v ^= from_lane_up<1>(v);
+        v ^= from_lane_up<2>(v);  // lane 0: Z_{-m}(fold) = raw(item)
+        if (tl == 0 && p_recf != kSortNone)
+        {
+            const uint32_t rec = p_recf & kSortRecMask;
+            if (!(p_recf & kSortMulti))
+                out[rec] = ~v;
+            else
+            {
+                // this piece's part: Z_{E - pe}(raw(piece)), E the record's end
+                const uint64_t E_rec = uint64_t(base) + off[rec] + len[rec];
+                v = zshift48(pow2, v, E_rec - p_pe);
+                __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
+    auto grab = [&]() {
+        uint32_t g = 0;
+        if (lane == 0) g = atomicAdd(&S.next_group, 1u);
+        return uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
+    };
+    auto load_desc = [&](uint32_t g) {
+        const uint32_t i = g * 8 + tw;
+        return *((g < n_groups && i < n_items) ? my_items + i : reinterpret_cast<const uint4*>(zero16));
+    };
+    // Uniform shape of a group: n rows (team 0's item, the largest, padded
+    // to an even count with a leading zero row), the first row of team 0's
+    // item, the last row in which some team's item starts (or its init word
+    // spills into), and the first row from which every lane reads item bytes
+    // (n: never, in a group with teams but no item).
+    struct Shape
+    {
+        int32_t n, fmin, fedge, fast;
+    };
+    auto shape_of = [&](const uint4& d, uint32_t g) {
+        Shape s{0, 0, 0, 0};
+        if (g >= n_groups) return s;
+        const int32_t rows0 = __builtin_amdgcn_readfirstlane(int(sort_rows(d)));
+        s.n = (rows0 + 1) & ~1;
+        s.fmin = s.n - rows0;
+        const uint32_t tlast = min(7u, n_items - 1 - g * 8);
+        s.fedge = s.n - __builtin_amdgcn_readlane(int(sort_rows(d)), int(tlast * kTeam)) + 1;
+        s.fast = tlast == 7 ? s.fedge + 1 : s.n;
+        return s;
+    };
+    auto row_ptr = [&](const SortView& v, int32_t r, bool fast) {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(v.p0 + uint64_t(uint32_t(r)) * kRowBytes);
+        if (!fast) p = (r >= v.lo && r <= v.hi) ? p : zero16;
+        return p;
+    };
+
+    uint32_t g_cur = grab();
+    uint4 d_cur = load_desc(g_cur);
+    uint32_t g_nxt = grab();
+    uint4 d_nxt = load_desc(g_nxt);
+    Shape sh = shape_of(d_cur, g_cur);
+    SortView cur = sort_view(d_cur, sh.n, tl, inits, zero_word, ones_word);
+    // Two-row ring: even rows in b0, odd rows in b1; each row step issues the
+    // next row (this group's, or row 0 of the next group) before folding the
+    // current one.  Groups have an even row count, so the roles never change.
+    // (Measured on the headline batch: one row ahead costs < 1 % against
+    // three; here it keeps the padding to half a row per group.)
+    uint4 b0 = load16(row_ptr(cur, 0, false)), b1;
+    __builtin_amdgcn_sched_barrier(0);
+    while (sh.n > 0)
+    {
+        const uint32_t g_nn = grab();
+        const uint4 d_nn = load_desc(g_nn);
+        const Shape shn = shape_of(d_nxt, g_nxt);
+        const SortView nxt = sort_view(d_nxt, shn.n, tl, inits, zero_word, ones_word);
+        uint32_t V[4] = {0, 0, 0, 0};
+        const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
+        // General row: padding skip, start mask and init word (rows up to
+        // fedge), end mask (row n - 1), zero-block reads.  Used for the first
+        // rows and the last two of a group; the rows between take the body
+        // loop below: all lanes read item bytes, nothing to mask.
+        auto gen_row = [&](uint4 d, int32_t r) {
+            if (r < fmin) return;  // the padding row: V stays 0
+            if (r <= fedge)
+            {
+                // row f: (d & keep) ^ ~init in one v_bitop3 per dword (truth
+                // table index S0 S1 S2 = d keep x, MSB first: 0x6A)
+                const bool at_f = r == cur.f;
+                d.x = at_f ? __builtin_amdgcn_bitop3_b32(d.x, cur.kf.x, cur.xf.x, 0x6A) : d.x;
+                d.y = at_f ? __builtin_amdgcn_bitop3_b32(d.y, cur.kf.y, cur.xf.y, 0x6A) : d.y;
+                d.z = at_f ? __builtin_amdgcn_bitop3_b32(d.z, cur.kf.z, cur.xf.z, 0x6A) : d.z;
+                d.w = at_f ? __builtin_amdgcn_bitop3_b32(d.w, cur.kf.w, cur.xf.w, 0x6A) : d.w;
+                d.x ^= r == cur.f + 1 ? cur.xs : 0u;
+            }
+            if (r == n - 1)
+            {
+                d.x &= cur.ke.x;
+                d.y &= cur.ke.y;
+                d.z &= cur.ke.z;
+                d.w &= cur.ke.w;
+            }
+            if (r == fmin)
+                row_first(V, d);  // team 0 starts here; every other team's row is zero
+            else
+                row_update(V, d, li);
+        };
+        // body rows [hend, n - 2): after every team's first row and init
+        // word (full groups only: a partial group has teams without items)
+        const int32_t hend = fast < n ? min(n - 2, (fedge + 2) & ~1) : n - 2;
+        int32_t r = 0;
+        for (; r < hend; r += 2)
+        {
+            b1 = load16(row_ptr(cur, r + 1, false));
+            __builtin_amdgcn_sched_barrier(0);
+            gen_row(b0, r);
+            b0 = load16(row_ptr(cur, r + 2, false));
+            __builtin_amdgcn_sched_barrier(0);
+            gen_row(b1, r + 1);
+        }
+        {
+            const uint8_t* pr = reinterpret_cast<const uint8_t*>(cur.p0);
+            for (; r < n - 2; r += 2)
+            {
+                b1 = load16(pr + uint32_t(r + 1) * uint32_t(kRowBytes));
+                __builtin_amdgcn_sched_barrier(0);
+                row_update(V, b0, li);
+                b0 = load16(pr + uint32_t(r + 2) * uint32_t(kRowBytes));
+                __builtin_amdgcn_sched_barrier(0);
+                row_update(V, b1, li);
+            }
+        }
+        b1 = load16(row_ptr(cur, n - 1, false));
+        __builtin_amdgcn_sched_barrier(0);
+        gen_row(b0, n - 2);
+        b0 = load16(row_ptr(nxt, 0, false));
+        __builtin_amdgcn_sched_barrier(0);
+        gen_row(b1, n - 1);
+        const uint32_t W = team_fold(V);
+        flush();  // the previous group's items
+        {
+            // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
+            const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
+            const uint32_t q = tl & 3u;
+            pz = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
+            p_recf = cur.recf;
+            p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;  // lane 0: the item's end
+        }
+        g_cur = g_nxt;
+        cur = nxt;
+        sh = shn;
+        g_nxt = g_nn;
+        d_nxt = d_nn;
+    }
+    flush();
+}
+
+hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint32_t* inits, uint64_t count, const SortedWorkspace& ws,
+                         uint32_t* out, const uint32_t* tables, const uint32_t* pow2, int grid,
+                         hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    const uint32_t nb = sorted_blocks(count);
+    const uint8_t* b = static_cast<const uint8_t*>(base);
+    hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
+                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables);
+    hipLaunchKernelGGL(crc32c_sorted_kernel, dim3(grid), dim3(kBlock), kLdsSorted, stream, b,
+                       offsets, lengths, inits, count, ws.blk_cost, nb, ws.ctrl, ws.items,
+                       ws.item_cap, out, tables, pow2);
+    return hipGetLastError();
+}
+
+uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes)
+{
+    return count + total_bytes / kSortPiece + 1;
+}
+
 // Allow the 152 KiB dynamic LDS image on the two persistent kernels.
 hipError_t configure_kernels()
 {
@@ -2197,6 +2833,9 @@ hipError_t configure_kernels()
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_sorted_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSorted);
     return e;
 }
 

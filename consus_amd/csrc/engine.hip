@@ -293,6 +293,7 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     DevBuf s_ctrl, s_R, s_snaps, s_pval;  // stream path (sorted batches)
+    DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
     PinBuf pin_small;                   // plan-size read-back, small host outputs
     PinBuf pin_stage, pin_out;          // packed small host batches: inputs, CRCs
     int ordinal = -1;
@@ -312,7 +313,8 @@ struct Ctx
     {
         if (stream) (void)hipStreamSynchronize(stream);
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
-                          &last_pos, &blk, &longs, &s_ctrl, &s_R, &s_snaps, &s_pval})
+                          &last_pos, &blk, &longs, &s_ctrl, &s_R, &s_snaps, &s_pval, &srt_cost,
+                          &srt_ctrl, &srt_items})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -428,6 +430,41 @@ int run_stream(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     return MI_CRC32C_OK;
 }
 
+// MI_CRC32C_VARPATH=pieces|sorted: the variable-length path for batches the
+// direct kernel does not take.  Default: the sorted path when the batch's
+// total bytes are known and at least kSortedMinBytes, else the piece path.
+// "sorted" takes it for every size with a known total (tests), "pieces" never.
+int varpath_forced()
+{
+    // read per batch (not cached) so that a test can switch paths in-process
+    const char* e = std::getenv("MI_CRC32C_VARPATH");
+    if (e && !std::strcmp(e, "pieces")) return 1;
+    if (e && !std::strcmp(e, "sorted")) return 2;
+    return 0;
+}
+
+// The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
+int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
+               const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
+{
+    const uint64_t cap = sorted_item_cap(count, total_bytes);
+    int st;
+    if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
+        (st = c->srt_ctrl.reserve(16)) || (st = c->srt_items.reserve(cap * 16)))
+        return st;
+    SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
+                       c->srt_items.as<uint4>(), c->srt_items.cap / 16};
+    // MI_CRC32C_SORTED_GRID=k: k workgroups instead of one per CU (tests: one
+    // workgroup puts every item of a small batch into one sorted list)
+    int grid = d->cus;
+    if (const char* e = std::getenv("MI_CRC32C_SORTED_GRID"))
+        grid = std::max(1, std::min(grid, std::atoi(e)));
+    HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
+                          c->stream));
+    mi_host::note_sorted_batch();
+    return MI_CRC32C_OK;
+}
+
 // MI_CRC32C_PLAN_SCAN=1: plans always take the separate scan pass (which
 // only plans of more than 16M records need), so tests exercise both forms.
 bool plan_scan_forced()
@@ -467,6 +504,9 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
                               c->stream));
         return MI_CRC32C_OK;
     }
+    if (total_bytes && count < kSortedMaxCount && varpath_forced() != 1 &&
+        (total_bytes >= kSortedMinBytes || varpath_forced() == 2))
+        return run_sorted(d, c, base, off, len, inits, count, total_bytes, out);
     const uint32_t nb = var_plan_blocks(count);
     int st;
     if ((st = c->blk.reserve((kBins * size_t(nb) + kPlanHdrWords) * 4)) ||

@@ -66,7 +66,8 @@ bool have_sse42()
 }
 #endif
 
-std::atomic<uint64_t> g_gpu_calls{0}, g_fb_calls{0}, g_fb_bytes{0}, g_sharded{0}, g_stream{0};
+std::atomic<uint64_t> g_gpu_calls{0}, g_fb_calls{0}, g_fb_bytes{0}, g_sharded{0}, g_stream{0},
+    g_sorted{0};
 std::atomic<int> g_fb_status{0};
 
 }  // namespace
@@ -107,6 +108,7 @@ void note_fallback(int status, uint64_t bytes)
 void note_gpu_call() { g_gpu_calls.fetch_add(1, std::memory_order_relaxed); }
 void note_sharded_call() { g_sharded.fetch_add(1, std::memory_order_relaxed); }
 void note_stream_batch() { g_stream.fetch_add(1, std::memory_order_relaxed); }
+void note_sorted_batch() { g_sorted.fetch_add(1, std::memory_order_relaxed); }
 
 }  // namespace mi_host
 
@@ -120,6 +122,7 @@ void mi_crc32c_stats(mi_crc32c_stats_t* out)
     out->fallback_bytes = mi_host::g_fb_bytes.load();
     out->sharded_calls = mi_host::g_sharded.load();
     out->stream_batches = mi_host::g_stream.load();
+    out->sorted_batches = mi_host::g_sorted.load();
     out->last_fallback_status = mi_host::g_fb_status.load();
     out->reserved = 0;
 }
@@ -131,6 +134,7 @@ void mi_crc32c_stats_reset(void)
     mi_host::g_fb_bytes.store(0);
     mi_host::g_sharded.store(0);
     mi_host::g_stream.store(0);
+    mi_host::g_sorted.store(0);
     mi_host::g_fb_status.store(0);
 }
 

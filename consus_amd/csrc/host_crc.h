@@ -29,5 +29,6 @@ void note_fallback(int status, uint64_t bytes);
 void note_gpu_call();
 void note_sharded_call();
 void note_stream_batch();
+void note_sorted_batch();
 
 }  // namespace mi_host

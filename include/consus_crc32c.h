@@ -87,6 +87,7 @@ typedef struct mi_crc32c_stats_t
     uint64_t stream_batches;      /* batches hashed by the stream path (records in order) */
     int32_t last_fallback_status; /* engine status that forced the last fallback (0: none) */
     int32_t reserved;
+    uint64_t sorted_batches;      /* variable-length batches hashed by the sorted path */
 } mi_crc32c_stats_t;
 void mi_crc32c_stats(mi_crc32c_stats_t* out);
 void mi_crc32c_stats_reset(void);

@@ -1,0 +1,216 @@
+"""GPU parity of the sorted variable-length path:
+one team per whole record, records binned by row count inside each
+workgroup's cost-balanced share, split records (> 64 KiB) XORed together
+from 64 KiB pieces.  Forced here with MI_CRC32C_VARPATH=sorted (the engine
+takes it by itself for batches of >= 64 MiB); every result is compared with
+the CPU oracle, bit-exact, and the path is checked to have run
+(mi_crc32c_stats().sorted_batches).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def sorted_path(engine):
+    old = os.environ.get("MI_CRC32C_VARPATH")
+    os.environ["MI_CRC32C_VARPATH"] = "sorted"
+    before = engine.stats()["sorted_batches"]
+    yield lambda: engine.stats()["sorted_batches"] - before
+    if old is None:
+        del os.environ["MI_CRC32C_VARPATH"]
+    else:
+        os.environ["MI_CRC32C_VARPATH"] = old
+
+
+def _packed(rng, lengths, gap=0, start=0):
+    offsets = np.zeros(lengths.size, dtype=np.uint64)
+    if lengths.size > 1:
+        steps = lengths[:-1].astype(np.uint64)
+        if gap:
+            steps = steps + rng.integers(0, gap + 1, lengths.size - 1).astype(np.uint64)
+        offsets[1:] = np.cumsum(steps)
+    offsets += np.uint64(start)
+    end = int(offsets[-1]) + int(lengths[-1]) if lengths.size else start
+    return offsets, end
+
+
+def _device_run(engine, buf, offsets, lengths, inits=None):
+    count = lengths.size
+    data = engine.DeviceBuffer(max(buf.size, 16))
+    data.upload(buf)
+    d_off, d_len, d_out = (engine.DeviceBuffer(max(count, 1) * 8), engine.DeviceBuffer(max(count, 1) * 4),
+                           engine.DeviceBuffer(max(count, 1) * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    d_in = None
+    if inits is not None:
+        d_in = engine.DeviceBuffer(count * 4)
+        d_in.upload(inits)
+    total = int(lengths.sum(dtype=np.uint64))
+    engine.device_batch(data, d_off, d_len, count, d_out, inits=d_in, total_bytes=max(total, 1))
+    got = d_out.download(np.uint32, count)
+    for b in (data, d_off, d_len, d_out, d_in):
+        if b is not None:
+            b.free()
+    return got
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_sorted_random_lengths(engine, oracle, sorted_path, seed):
+    """Lengths 0..20000 (including 0-3 B records, finished by the cost
+    kernel), unaligned starts, small gaps, with and without inits."""
+    rng = np.random.default_rng(100 + seed)
+    count = 40_000
+    lengths = rng.integers(0, 20_000, count).astype(np.uint32)
+    lengths[rng.integers(0, count, 2000)] = rng.integers(0, 5, 2000)
+    offsets, end = _packed(rng, lengths, gap=9, start=int(rng.integers(0, 128)))
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+    assert sorted_path() == 2
+
+
+def test_sorted_zipf_host_and_device(engine, oracle, sorted_path):
+    """configs[2]'s length distribution (Zipf 64 B - 64 KiB), packed, as a
+    device batch and as a host batch (staged)."""
+    rng = np.random.default_rng(5)
+    count = 30_000
+    lengths = engine.zipf_lengths(0xDA7A5EED, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    exp = oracle.batch(buf, offsets, lengths)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths), exp)
+    assert np.array_equal(engine.crc32c_batch(buf, offsets, lengths, planned=True), exp)
+    assert sorted_path() == 2
+
+
+@pytest.mark.parametrize("start", [0, 1, 64, 127])
+def test_sorted_split_records(engine, oracle, sorted_path, start):
+    """Records around and beyond the 64 KiB piece: 65535, 65536, 65537,
+    65536 + 127/128/129, 200 KiB, 1 MiB, 3 MiB at every alignment class,
+    mixed with short ones; inits chain through the first piece."""
+    rng = np.random.default_rng(40 + start)
+    big = [65535, 65536, 65537, 65536 + 127, 65536 + 128, 65536 + 129, 131072, 131073,
+           200 << 10, 1 << 20, 3 << 20, 4, 5, 3, 0, 1000]
+    lengths = np.array(big * 3 + list(rng.integers(0, 9000, 300)), dtype=np.uint32)
+    rng.shuffle(lengths)
+    offsets, end = _packed(rng, lengths, gap=3, start=start)
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+
+
+@pytest.mark.parametrize("grid", ["1", "3"])
+def test_sorted_one_workgroup_mixed_groups(engine, oracle, sorted_path, grid):
+    """One (or three) workgroups: every item of the batch in one sorted list,
+    so groups mix pieces of one record with short items and row counts far
+    apart (a 1-row last piece beside a 513-row piece: rows before the item's
+    first row must stay zero, init word included)."""
+    rng = np.random.default_rng(int(grid))
+    lengths = np.array([65537, 65536 + 60000, 131073, 5, 100, 4000, 65535, 200 << 10] +
+                       list(rng.integers(0, 3000, 40)), dtype=np.uint32)
+    rng.shuffle(lengths)
+    offsets, end = _packed(rng, lengths, gap=7, start=3)
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    os.environ["MI_CRC32C_SORTED_GRID"] = grid
+    try:
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                              oracle.batch(buf, offsets, lengths))
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                              oracle.batch(buf, offsets, lengths, inits))
+    finally:
+        del os.environ["MI_CRC32C_SORTED_GRID"]
+
+
+def test_sorted_one_huge_record(engine, oracle, sorted_path):
+    """One 40 MiB record and a few short ones: the record's 641 pieces are
+    spread over many workgroups (the cost split falls inside it)."""
+    rng = np.random.default_rng(9)
+    lengths = np.array([17, 40 << 20, 300, 5], dtype=np.uint32)
+    offsets, end = _packed(rng, lengths, start=3)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    inits = np.array([1, 0xDEADBEEF, 7, 9], dtype=np.uint32)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+
+
+@pytest.mark.parametrize("count", [1, 2, 7, 8, 9, 255, 257, 4097])
+def test_sorted_few_records(engine, oracle, sorted_path, count):
+    """Fewer records than workgroups (most ranges empty) and partial groups."""
+    rng = np.random.default_rng(count)
+    lengths = rng.integers(4, 5000, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths, gap=40, start=5)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+
+
+def test_sorted_only_tiny_records(engine, oracle, sorted_path):
+    """Every record shorter than 4 B: the cost kernel finishes them all and
+    the hash kernel has no items (total cost 0)."""
+    rng = np.random.default_rng(11)
+    count = 10_000
+    lengths = rng.integers(0, 4, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths, gap=2)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+
+
+def test_sorted_unordered_overlapping(engine, oracle, sorted_path):
+    """Records in any order, overlapping each other, equal lengths (large
+    bins of one row count)."""
+    rng = np.random.default_rng(13)
+    buf = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    count = 20_000
+    lengths = np.where(rng.random(count) < 0.5, 4096, rng.integers(0, 70_000, count)).astype(np.uint32)
+    offsets = rng.integers(0, buf.size - 70_000, count).astype(np.uint64)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+
+
+def test_sorted_matches_piece_path(engine, oracle):
+    """The two variable-length paths agree on the same device batch."""
+    rng = np.random.default_rng(17)
+    count = 50_000
+    lengths = engine.zipf_lengths(0x5EED, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths, gap=5, start=33)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    old = os.environ.get("MI_CRC32C_VARPATH")
+    try:
+        os.environ["MI_CRC32C_VARPATH"] = "pieces"
+        a = _device_run(engine, buf, offsets, lengths)
+        os.environ["MI_CRC32C_VARPATH"] = "sorted"
+        b = _device_run(engine, buf, offsets, lengths)
+    finally:
+        if old is None:
+            os.environ.pop("MI_CRC32C_VARPATH", None)
+        else:
+            os.environ["MI_CRC32C_VARPATH"] = old
+    assert np.array_equal(a, b)
+    assert np.array_equal(b, oracle.batch(buf, offsets, lengths))
+
+
+def test_sorted_default_for_large_batches(engine, oracle):
+    """Without the knob, a batch of >= 64 MiB takes the sorted path."""
+    rng = np.random.default_rng(19)
+    count = 20_000
+    lengths = rng.integers(3000, 4000, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    before = engine.stats()["sorted_batches"]
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+    assert engine.stats()["sorted_batches"] == before + 1
