@@ -63,18 +63,40 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 __device__ __forceinline__ void stage_tables(const uint32_t* __restrict__ g)
 {
     if (MI_CRC_ABLATE & 1) return;
-    for (uint32_t i = threadIdx.x; i < 1024u * 8u; i += blockDim.x)
+    // Every record kernel runs kBlock threads: all loads are issued first,
+    // then all stores (one L2 round trip per thread, not one per iteration).
+    constexpr uint32_t NM = 1024u * 8u / kBlock;          // G^{128} entries x 8 quads
+    constexpr uint32_t NT = (4096u + 2048u) / 4u;         // T_0..15, G^32, G^64 as uint4
+    constexpr uint32_t NTI = (NT + kBlock - 1) / kBlock;
+    static_assert(1024u * 8u % kBlock == 0, "table staging shape");
+    uint32_t v[NM];
+    uint4 t[NTI];
+    const uint4* src = reinterpret_cast<const uint4*>(g + kTabT);
+#pragma unroll
+    for (uint32_t k = 0; k < NM; ++k) v[k] = g[kTabMain + ((threadIdx.x + k * kBlock) >> 3)];
+#pragma unroll
+    for (uint32_t k = 0; k < NTI; ++k)
     {
+        const uint32_t i = threadIdx.x + k * kBlock;
+        t[k] = i < NT ? src[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < NM; ++k)
+    {
+        const uint32_t i = threadIdx.x + k * kBlock;
         const uint32_t e = i >> 3;          // t * 256 + b
         const uint32_t c4 = (i & 7u) * 4u;  // first of 4 consecutive copies
-        const uint32_t t = e >> 8, b = e & 255u;
-        const uint32_t v = g[kTabMain + e];
-        const uint32_t addr = (t >> 1) * 65536u + b * 256u + (t & 1u) * 128u + c4 * 4u;
-        *reinterpret_cast<uint4*>(smem + kLdsMain + addr) = make_uint4(v, v, v, v);
+        const uint32_t tb = e >> 8, b = e & 255u;
+        const uint32_t addr = (tb >> 1) * 65536u + b * 256u + (tb & 1u) * 128u + c4 * 4u;
+        *reinterpret_cast<uint4*>(smem + kLdsMain + addr) = make_uint4(v[k], v[k], v[k], v[k]);
     }
-    const uint4* src = reinterpret_cast<const uint4*>(g + kTabT);
     uint4* dst = reinterpret_cast<uint4*>(smem + kLdsT);
-    for (uint32_t i = threadIdx.x; i < (4096u + 2048u) / 4u; i += blockDim.x) dst[i] = src[i];
+#pragma unroll
+    for (uint32_t k = 0; k < NTI; ++k)
+    {
+        const uint32_t i = threadIdx.x + k * kBlock;
+        if (i < NT) dst[i] = t[k];
+    }
     __syncthreads();
 }
 
@@ -2199,6 +2221,14 @@ constexpr uint32_t kSortFirst = 0x40000000u;  // ... its first piece (carries th
 constexpr uint32_t kSortRecMask = 0x3FFFFFFFu;
 constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
 
+// measurement builds only: MI_SORT_STAMP=1 records s_memrealtime stamps
+// (100 MHz) per wave into the item workspace past item_cap, 8 words: start,
+// end of the prologue, end of the last group, then after the table staging,
+// the block search, the boundaries, binning pass 1 and the item allocation
+// (tools/sorted_stamps.py)
+#ifndef MI_SORT_STAMP
+#define MI_SORT_STAMP 0
+#endif
 // measurement builds only (tools/build_variant.sh), results are wrong: stop
 // after the binning (1), the block search (2), the boundaries (3), the
 // table staging (4): times the prologue's phases
@@ -2283,9 +2313,11 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
 // LDS of the sorted kernel beyond the table image.
 struct SortShared
 {
-    uint32_t bins[kSortBins];  // item counts per bin, then their cursors
+    uint32_t bins[kSortBins];  // whole records / last pieces per bin, then bin bases
+    uint32_t fbins[2];         // full pieces of split records with 513 / 512 rows
     uint32_t n_items;
-    uint32_t item_base;
+    uint32_t n_full;           // full pieces (listed first: the largest items)
+    uint32_t full_base;        // their slots: items[count + full_base ...]
     uint32_t next_group;
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
@@ -2329,17 +2361,18 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* wsum
 }
 
 // Wave 0: the total cost C, the targets C b / G and C (b + 1) / G, and the
-// cost blocks holding them (each lane takes 16 consecutive blocks per round,
-// so 1,024 blocks cost one round trip).
+// cost blocks holding them.  Each lane takes 16 consecutive blocks per round;
+// up to 1,024 blocks (1M records) the costs stay in registers, so the total
+// and the search cost one round trip.
 __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ blk_cost, uint32_t nb,
                                                  uint64_t count, SortShared& S)
 {
     constexpr uint32_t K = 16;
     const uint32_t lane = threadIdx.x & 63u;
-    uint64_t tot = 0;
+    const bool one_round = nb <= 64 * K;
+    uint64_t v[K], tot = 0;
     for (uint32_t c0 = 0; c0 < nb; c0 += 64 * K)
     {
-        uint64_t v[K];
 #pragma unroll
         for (uint32_t k = 0; k < K; ++k)
         {
@@ -2367,12 +2400,12 @@ __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ bl
     uint64_t carry = 0;
     for (uint32_t c0 = 0; c0 < nb && !(found[0] && found[1]); c0 += 64 * K)
     {
-        uint64_t v[K], sum = 0;
+        uint64_t sum = 0;
 #pragma unroll
         for (uint32_t k = 0; k < K; ++k)
         {
             const uint32_t j = c0 + lane * K + k;
-            v[k] = j < nb ? blk_cost[j] : 0;
+            if (!one_round) v[k] = j < nb ? blk_cost[j] : 0;
             sum += v[k];
         }
         const uint64_t incl = carry + wave_incl_scan64(sum), excl = incl - sum;
@@ -2532,63 +2565,121 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint32_t lane = threadIdx.x & 63u;
+    uint64_t* const stamps = reinterpret_cast<uint64_t*>(items + item_cap) +
+                             (uint64_t(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64) * 8;
+    if (MI_SORT_STAMP && lane == 0) stamps[0] = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = 0;
+    if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     stage_tables(tables);  // ends with a barrier
+    if (MI_SORT_STAMP && lane == 0) stamps[3] = __builtin_amdgcn_s_memrealtime();
     if (MI_SORT_STOP == 4) return;
 
     // (1) Wave 0: the two targets and the cost blocks holding them.
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
+    if (MI_SORT_STAMP && lane == 0) stamps[4] = __builtin_amdgcn_s_memrealtime();
     if (MI_SORT_STOP == 2) return;
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S);
+    if (MI_SORT_STAMP && lane == 0) stamps[5] = __builtin_amdgcn_s_memrealtime();
     if (MI_SORT_STOP == 3) return;
 
-    // (3) Bin the items by row count (pass 1), place the bins largest first,
-    // write the descriptors (pass 2).  Whole records and last pieces take one
-    // LDS atomic per distinct row count of a wave (match_key10); the full
-    // pieces of split records one per record.
+    // (3) Bin the items by row count, largest first.  Whole records and the
+    // last pieces of split records go to this workgroup's slots of the
+    // record-indexed list, items[rlo ...] (a record has one last piece, so the
+    // ranges never overlap); the full 64 KiB pieces of split records, 512 or
+    // 513 rows, to slots taken from ctrl[0] past items[count] and are listed
+    // first.  Ranks come from returning LDS atomics: one per distinct row
+    // count of a wave (match_key10).  Up to 8 records per thread the ranks
+    // stay in registers and the descriptors are written after the bin scan;
+    // larger ranges take a second pass over the records.
     const uint32_t rlo = S.bound[0], klo0 = S.bound[1], rhi = S.bound[2], khi0 = S.bound[3];
     const uint64_t rend = min(uint64_t(rhi) + (khi0 ? 1u : 0u), count);
-    auto bin_pass = [&](uint4* my_items) {
-        for (uint64_t r = uint64_t(rlo) + threadIdx.x; r < rend; r += kBlock)
+    constexpr uint32_t U = 4, CH = 2;  // records per thread per chunk, chunks held
+    const bool held = rend <= uint64_t(rlo) + U * CH * kBlock;
+    struct RecInfo
+    {
+        SortCost s;
+        uint32_t klo, nf;
+        bool last;
+    };
+    auto info = [&](uint64_t r, uint64_t a, uint32_t L) {
+        RecInfo f;
+        f.s = sort_cost(a, L);  // L = 0 past rend: no items
+        f.klo = r == rlo ? klo0 : 0u;
+        const uint32_t khi = r == rhi ? khi0 : f.s.n;
+        const uint32_t lim = f.s.n ? f.s.n - 1 : 0u;  // pieces before the last
+        f.nf = min(khi, lim) > f.klo ? min(khi, lim) - f.klo : 0u;
+        f.last = f.s.n != 0 && f.klo < khi && khi == f.s.n;
+        return f;
+    };
+    // one returning atomic per full-piece run and per wave leader of a row
+    // count; returns (full rank or cursor, last-piece rank or cursor)
+    auto take = [&](const RecInfo& f, uint32_t& rf, uint32_t& rl) {
+        rf = f.nf ? atomicAdd(&S.fbins[f.s.rows_full == kSortRows ? 0 : 1], f.nf) : 0u;
+        const uint32_t key = kSortRows - f.s.rows_last;
+        const uint64_t eq = match_key10(key, f.last);
+        const uint32_t rank = uint32_t(__builtin_popcountll(eq & ((uint64_t(1) << lane) - 1)));
+        uint32_t b0 = 0;
+        if (f.last && rank == 0) b0 = atomicAdd(&S.bins[key], uint32_t(__builtin_popcountll(eq)));
+        b0 = uint32_t(__shfl(int(b0), f.last ? int(__builtin_ctzll(eq)) : int(lane)));
+        rl = b0 + rank;
+    };
+    auto desc = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t k) {
+        const uint64_t ps = a + uint64_t(k) * kSortPiece;
+        const uint32_t pl = uint32_t(min<uint64_t>(kSortPiece, a + L - ps));
+        return make_uint4(uint32_t(ps), uint32_t(ps >> 32), pl,
+                          uint32_t(r) | (f.s.n > 1 ? kSortMulti : 0u) | (k == 0 ? kSortFirst : 0u));
+    };
+    uint4* const fullv = items + count;
+    uint4* const lastv = items + rlo;
+    // absolute slots: full run at fpos, last piece at lpos
+    auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
+        for (uint32_t i = 0; i < f.nf; ++i) fullv[S.full_base + fpos + i] = desc(r, a, L, f, f.klo + i);
+        if (f.last) lastv[lpos] = desc(r, a, L, f, f.s.n - 1);
+    };
+    uint64_t ha[CH][U];
+    uint32_t hL[CH][U], hf[CH][U], hl[CH][U];
+    auto pass = [&](bool second) {
+        for (uint32_t c = 0;; ++c)
         {
-            const uint64_t a = uint64_t(base) + off[r];
-            const uint32_t L = len[r];
-            const SortCost s = sort_cost(a, L);
-            const uint32_t klo = r == rlo ? klo0 : 0u;
-            const uint32_t khi = r == rhi ? khi0 : s.n;
-            const uint32_t lim = s.n ? s.n - 1 : 0u;  // pieces before the last
-            const uint32_t nf = min(khi, lim) > klo ? min(khi, lim) - klo : 0u;
-            const bool last = s.n != 0 && klo < khi && khi == s.n;
-            const uint32_t flags = s.n > 1 ? kSortMulti : 0u;
-            auto desc = [&](uint32_t k) {
-                const uint64_t ps = a + uint64_t(k) * kSortPiece;
-                const uint32_t pl = uint32_t(min<uint64_t>(kSortPiece, a + L - ps));
-                return make_uint4(uint32_t(ps), uint32_t(ps >> 32), pl,
-                                  uint32_t(r) | flags | (k == 0 ? kSortFirst : 0u));
-            };
-            if (nf)
+            const uint64_t c0 = uint64_t(rlo) + threadIdx.x + uint64_t(c) * U * kBlock;
+            if (c0 >= rend) break;
+            uint64_t av[U];
+            uint32_t Lv[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
             {
-                const uint32_t p = atomicAdd(&S.bins[kSortRows - s.rows_full], nf);
-                if (my_items)
-                    for (uint32_t i = 0; i < nf; ++i) my_items[p + i] = desc(klo + i);
+                const uint64_t r = c0 + u * kBlock;
+                av[u] = r < rend ? uint64_t(base) + off[r] : 0;
+                Lv[u] = r < rend ? len[r] : 0;
             }
-            const uint32_t key = kSortRows - s.rows_last;
-            const uint64_t eq = match_key10(key, last);
-            const uint32_t rank = uint32_t(__builtin_popcountll(eq & ((uint64_t(1) << lane) - 1)));
-            uint32_t pos = 0;
-            if (last && rank == 0) pos = atomicAdd(&S.bins[key], uint32_t(__builtin_popcountll(eq)));
-            if (my_items)
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
             {
-                pos = uint32_t(__shfl(int(pos), last ? int(__builtin_ctzll(eq)) : int(lane)));
-                if (last) my_items[pos + rank] = desc(s.n - 1);
+                const uint64_t r = c0 + u * kBlock;
+                const RecInfo f = info(r, av[u], Lv[u]);
+                uint32_t rf, rl;
+                take(f, rf, rl);
+                if (second)
+                    place(r, av[u], Lv[u], f, rf, rl);  // the bins hold cursors now
+                else if (held)
+#pragma unroll
+                    for (uint32_t cc = 0; cc < CH; ++cc)
+                        if (cc == c)
+                        {
+                            ha[cc][u] = av[u];
+                            hL[cc][u] = Lv[u];
+                            hf[cc][u] = rf;
+                            hl[cc][u] = rl;
+                        }
             }
         }
     };
-    bin_pass(nullptr);
+    pass(false);
     __syncthreads();
+    if (MI_SORT_STAMP && lane == 0) stamps[6] = __builtin_amdgcn_s_memrealtime();
     {
         const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
         uint64_t total;
@@ -2596,24 +2687,55 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = e;
         if (threadIdx.x == 0)
         {
-            S.n_items = uint32_t(total);
-            uint32_t b = __hip_atomic_fetch_add(ctrl, uint32_t(total), __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-            if (uint64_t(b) + total > item_cap)
+            const uint32_t nf = S.fbins[0] + S.fbins[1];
+            uint32_t fb = 0;
+            if (nf)  // split records only
+                fb = __hip_atomic_fetch_add(ctrl, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.n_full = nf;
+            S.n_items = nf + uint32_t(total);
+            if (count + uint64_t(fb) + nf > item_cap)
             {
                 ctrl[1] = 1;  // workspace too small (understated total_bytes): out[] left alone
                 S.n_items = 0;
             }
-            S.item_base = b;
+            S.full_base = fb;
+            if (!held)  // cursors for the second pass
+            {
+                S.fbins[1] = S.fbins[0];
+                S.fbins[0] = 0;
+            }
         }
     }
     __syncthreads();
-    uint4* const my_items = items + S.item_base;
-    const uint32_t n_items = S.n_items;
-    if (n_items) bin_pass(my_items);
+    if (MI_SORT_STAMP && lane == 0) stamps[7] = __builtin_amdgcn_s_memrealtime();
+    const uint32_t n_items = S.n_items, n_full = S.n_full;
+    if (n_items)
+    {
+        if (held)
+        {
+            const uint32_t f513 = S.fbins[0];
+#pragma unroll
+            for (uint32_t c = 0; c < CH; ++c)
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u)
+                {
+                    const uint64_t r = uint64_t(rlo) + threadIdx.x + (uint64_t(c) * U + u) * kBlock;
+                    if (r < rend)
+                    {
+                        const RecInfo f = info(r, ha[c][u], hL[c][u]);
+                        const uint32_t fpos = (f.s.rows_full == kSortRows ? 0u : f513) + hf[c][u];
+                        place(r, ha[c][u], hL[c][u], f, fpos,
+                              f.last ? S.bins[kSortRows - f.s.rows_last] + hl[c][u] : 0u);
+                    }
+                }
+        }
+        else
+            pass(true);
+    }
     __syncthreads();
     if (n_items == 0 || MI_SORT_STOP == 1) return;
 
+    if (MI_SORT_STAMP && lane == 0) stamps[1] = __builtin_amdgcn_s_memrealtime();
     // (4) Groups of 8 items, largest first, one LDS grab per group.
     const uint32_t n_groups = (n_items + 7) / 8;
     const uint32_t tl = threadIdx.x & (kTeam - 1);
@@ -2653,9 +2775,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         if (lane == 0) g = atomicAdd(&S.next_group, 1u);
         return uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
     };
+    const uint4* const listF = items + count + S.full_base;  // full pieces first
+    const uint4* const listL = items + rlo - n_full;          // then the rest
     auto load_desc = [&](uint32_t g) {
         const uint32_t i = g * 8 + tw;
-        return *((g < n_groups && i < n_items) ? my_items + i : reinterpret_cast<const uint4*>(zero16));
+        return *((g < n_groups && i < n_items) ? (i < n_full ? listF : listL) + i
+                                               : reinterpret_cast<const uint4*>(zero16));
     };
     // Uniform shape of a group: n rows (team 0's item, the largest, padded
     // to an even count with a leading zero row), the first row of team 0's
@@ -2781,6 +2906,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         d_nxt = d_nn;
     }
     flush();
+    if (MI_SORT_STAMP && lane == 0) stamps[2] = __builtin_amdgcn_s_memrealtime();
 }
 
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,

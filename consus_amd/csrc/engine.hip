@@ -443,17 +443,22 @@ int varpath_forced()
     return 0;
 }
 
+// The stamp area of the last sorted batch (MI_SORT_STAMP measurement builds).
+uint64_t* last_sorted_stamps = nullptr;
+
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
 int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
 {
     const uint64_t cap = sorted_item_cap(count, total_bytes);
     int st;
+    // + a stamp area for MI_SORT_STAMP measurement builds (8 words per wave)
     if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
-        (st = c->srt_ctrl.reserve(16)) || (st = c->srt_items.reserve(cap * 16)))
+        (st = c->srt_ctrl.reserve(16)) || (st = c->srt_items.reserve(cap * 16 + 65536 * 64)))
         return st;
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
-                       c->srt_items.as<uint4>(), c->srt_items.cap / 16};
+                       c->srt_items.as<uint4>(), (c->srt_items.cap - 65536 * 64) / 16};
+    last_sorted_stamps = reinterpret_cast<uint64_t*>(ws.items + ws.item_cap);
     // MI_CRC32C_SORTED_GRID=k: k workgroups instead of one per CU (tests: one
     // workgroup puts every item of a small batch into one sorted list)
     int grid = d->cus;
@@ -1115,6 +1120,10 @@ int mi_memset(void* dev, int value, size_t bytes)
     HIP_TRY(hipStreamSynchronize(c->stream));
     return MI_CRC32C_OK;
 }
+
+// Dev tool (not in the public header): the stamp area of the calling
+// thread's last sorted batch, 8 x u64 per wave, MI_SORT_STAMP builds only.
+void* mi_dev_sorted_stamps(void) { return last_sorted_stamps; }
 
 int mi_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t byte_offset)
 {

@@ -133,6 +133,25 @@ def test_sorted_one_workgroup_mixed_groups(engine, oracle, sorted_path, grid):
         del os.environ["MI_CRC32C_SORTED_GRID"]
 
 
+@pytest.mark.parametrize("grid", ["1", "2"])
+def test_sorted_second_pass(engine, oracle, sorted_path, grid):
+    """More than 8 records per thread in a workgroup's range (one or two
+    workgroups for 30K records): the binning takes its second pass instead
+    of holding the ranks in registers; split records included."""
+    rng = np.random.default_rng(50 + int(grid))
+    lengths = rng.integers(0, 3000, 30_000).astype(np.uint32)
+    lengths[rng.integers(0, lengths.size, 12)] = rng.integers(65_537, 300_000, 12)
+    offsets, end = _packed(rng, lengths, gap=5, start=11)
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    os.environ["MI_CRC32C_SORTED_GRID"] = grid
+    try:
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                              oracle.batch(buf, offsets, lengths, inits))
+    finally:
+        del os.environ["MI_CRC32C_SORTED_GRID"]
+
+
 def test_sorted_one_huge_record(engine, oracle, sorted_path):
     """One 40 MiB record and a few short ones: the record's 641 pieces are
     spread over many workgroups (the cost split falls inside it)."""
