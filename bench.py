@@ -130,7 +130,8 @@ def pmc_traffic(args) -> tuple[float | None, str]:
     except Exception as e:  # noqa: BLE001 -- traffic is optional, the bench is not
         return None, f"rocprofv3 pass failed: {e}"
     fixed = args.config in ("fixed4k", "single")  # single: the same code on its 4 KiB chunks
-    step_kernels = ("plan_", "long_items", "crc32c_chunk_kernel", "crc32c_finalize", "long_finalize")
+    step_kernels = ("sorted_cost_kernel", "crc32c_sorted_kernel",  # the sorted path
+                    "plan_", "long_items", "crc32c_chunk_kernel", "crc32c_finalize", "long_finalize")
     vals = []
     for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
@@ -346,6 +347,7 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
         for _ in range(args.warmup):
             E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
         E.sync()
+        sorted0 = E.stats().get("sorted_batches", 0)
         t0 = time.perf_counter()
         E.timer_start()
         for _ in range(args.steps):
@@ -355,6 +357,7 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
         dig = E.crc32c_device(out, R * 4)
         g = gold.get("zipf_seed0x5eed_data0xda7a5eed_1048576", {})
         achieved = total / (ev * 1e-3) / 1e9
+        on_sorted = E.stats().get("sorted_batches", 0) - sorted0 == args.steps
         res.update({
             "metric": "GiB/s CRC32C over device-resident mixed-length records (Zipf 64 B-64 KiB)",
             "value": round(total / (wall) / 2**30, 2), "unit": "GiB/s",
@@ -367,7 +370,9 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
                          "traffic": None if traffic[0] is None else round(traffic[0]),
                          "traffic_note": traffic[1], "algorithmic_bytes": total,
                          "step_ms_events": round(ev, 4),
-                         "kernel": "plan + crc32c_chunk_kernel + finalize (whole step)"},
+                         "kernel": ("sorted_cost_kernel + crc32c_sorted_kernel (whole step, "
+                                    "sorted path)") if on_sorted else
+                                   "plan + crc32c_chunk_kernel + finalize (whole step, piece path)"},
             "digest_verified": (dig == g.get("digest")) if g and R == 1 << 20 else None,
             "digests": [f"{dig:#010x}"]})
         return res

@@ -2895,7 +2895,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
             const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
             const uint32_t q = tl & 3u;
-            pz = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
+            uint32_t pz_new = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
+            // an opaque definition: without it the loop-carried copy of pz at the
+            // loop header waited for this load (and the ring's row 0) every group
+            asm volatile("" : "+v"(pz_new));
+            pz = pz_new;
             p_recf = cur.recf;
             p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;  // lane 0: the item's end
         }
