@@ -36,7 +36,9 @@ constexpr int kTabZero = kTabZInv128 + 1024;    // 4 zero words (init 0 when ini
 constexpr int kTabFInit = kTabZero + 4;         // Z_n(0xFFFFFFFF), n = 0..4096 (init 0 seeds)
 constexpr int kTabZRows = kTabFInit + 4100;     // G^{128 k}, k = 1..32 (last-piece shifts)
 constexpr int kTabZNeg = kTabZRows + 32 * 1024; // Z_{-m} = (Z_m)^{-1}, m = 0..127 (direct kernel)
-constexpr int kTabWords = kTabZNeg + 128 * 1024;
+constexpr int kTabLane = kTabZNeg + 128 * 1024; // Z_16, Z_12, Z_8, Z_4, Z_32, Z_64 as six 64-entry
+                                                 // tables each: [op][c][i] = Z(i << 6c) (lane fold)
+constexpr int kTabWords = kTabLane + 6 * 6 * 64;
 
 // LDS image of the record kernels (bytes).
 constexpr uint32_t kLdsMain = 0;            // 128 KiB bank-private G^{128}

@@ -190,13 +190,71 @@ __device__ __forceinline__ uint32_t from_lane_up(uint32_t v)
     return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x100 + N, 0xF, 0xF, true));
 }
 
+#ifndef MI_FOLD_MASK
+#define MI_FOLD_MASK 0
+#endif
 __device__ __forceinline__ uint32_t team_fold(const uint32_t (&V)[4])
 {
     if (MI_CRC_ABLATE & 16) return V[0] ^ V[1] ^ V[2] ^ V[3];
     const uint32_t x = zT<4>(V[0]) ^ zT<3>(V[1]) ^ zT<2>(V[2]) ^ zT<1>(V[3]);
+#if MI_FOLD_MASK
+    // the tree's lookups only in the lanes whose result is used (fewer lanes
+    // per ds_read_b32, fewer bank conflicts); the DPP reads stay unmasked
+    const uint32_t u1 = from_lane_up<1>(x);
+    uint32_t y = 0, w = 0, r = 0;
+    if (!(threadIdx.x & 1u)) y = zT<4>(x) ^ u1;
+    const uint32_t u2 = from_lane_up<2>(y);
+    if (!(threadIdx.x & 3u)) w = zG(kLdsZ32, y) ^ u2;
+    const uint32_t u4 = from_lane_up<4>(w);
+    if (!(threadIdx.x & 7u)) r = zG(kLdsZ64, w) ^ u4;
+    return r;
+#else
     const uint32_t y = zT<4>(x) ^ from_lane_up<1>(x);
     const uint32_t w = zG(kLdsZ32, y) ^ from_lane_up<2>(y);
     return zG(kLdsZ64, w) ^ from_lane_up<4>(w);
+#endif
+}
+
+// The same fold without LDS tables (MI_FOLD_LANE): every Z_n of the fold is
+// six 64-entry tables of 6-bit slices (kTabLane), each held one entry per lane
+// in a VGPR and read with ds_bpermute, a crossbar permute that touches no LDS
+// bank.  The shared slice-by-16 tables cannot be made bank-private (24 KiB of
+// them beside the 128 KiB G^{128} image), so their random lookups conflict
+// 3.5-way on average; these cannot conflict.  The permute uses address bits
+// 7:2 only, so each slice's address is one shift.  Costs 36 VGPRs.
+#ifndef MI_FOLD_LANE
+#define MI_FOLD_LANE 1
+#endif
+struct LaneTabs
+{
+    uint32_t t[36];
+};
+__device__ __forceinline__ void load_lane_tabs(LaneTabs& L, const uint32_t* __restrict__ tables)
+{
+    const uint32_t* p = tables + kTabLane + (threadIdx.x & 63u);
+#pragma unroll
+    for (int k = 0; k < 36; ++k) L.t[k] = p[k * 64];
+}
+__device__ __forceinline__ uint32_t bperm(uint32_t addr, uint32_t tab)
+{
+    return uint32_t(__builtin_amdgcn_ds_bpermute(int(addr), int(tab)));
+}
+template <int K>
+__device__ __forceinline__ uint32_t zL(const LaneTabs& L, uint32_t v)
+{
+    const uint32_t* z = L.t + 6 * K;
+    return xor3(xor3(bperm(v << 2, z[0]), bperm(v >> 4, z[1]), bperm(v >> 10, z[2])),
+                bperm(v >> 16, z[3]), bperm(v >> 22, z[4])) ^
+           bperm(v >> 28, z[5]);
+}
+// Every lane of the wave must be active (ds_bpermute reads inactive lanes as 0).
+__device__ __forceinline__ uint32_t team_fold_lane(const uint32_t (&V)[4], const LaneTabs& L)
+{
+    if (MI_CRC_ABLATE & 16) return V[0] ^ V[1] ^ V[2] ^ V[3];
+    const uint32_t x = zL<0>(L, V[0]) ^ zL<1>(L, V[1]) ^ zL<2>(L, V[2]) ^ zL<3>(L, V[3]);
+    const uint32_t y = zL<0>(L, x) ^ from_lane_up<1>(x);
+    const uint32_t w = zL<4>(L, y) ^ from_lane_up<2>(y);
+    return zL<5>(L, w) ^ from_lane_up<4>(w);
 }
 
 // Record bytes are read exactly once: non-temporal loads (global_load_dwordx4
@@ -347,6 +405,10 @@ __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uin
     constexpr int SG = G * kGroupRows / Q;  // sub-groups per record
     static_assert(G * kGroupRows % Q == 0 && SG % NB == 0 && NB >= 2, "pipeline shape");
     stage_tables(tables);
+#if MI_FOLD_LANE
+    LaneTabs lt;
+    load_lane_tabs(lt, tables);
+#endif
 
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t li = lane_info();
@@ -403,7 +465,11 @@ __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uin
                     row_update(V, cur[r], li);
             }
         }
+#if MI_FOLD_LANE
+        const uint32_t raw = team_fold_lane(V, lt);
+#else
         const uint32_t raw = team_fold(V);
+#endif
         if (tl == 0 && team + it * nteams < count) out[rec] = ~raw;
         rec = next;
         if (INITS) init_word = next_init;
@@ -2193,7 +2259,7 @@ hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32
 // ---------------------------------------------------------------------------
 // Variable-length batches, sorted path: one team per
 // whole record, records binned by row count inside each workgroup's share.
-//   sorted_cost_kernel:   per block of 4,096 records, the sum of the records'
+//   sorted_cost_kernel:   per block of 1,024 records, the sum of the records'
 //       costs (rows plus a fold allowance per item).  Records shorter than
 //       4 B are finished here byte-serially; split records get out[r] = ~0.
 //   crc32c_sorted_kernel: with C the total cost and G workgroups, workgroup b
@@ -2202,8 +2268,8 @@ hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32
 //       first), writes 16-B descriptors to the workspace, and its 16 waves
 //       take groups of 8 items (one per team) from an LDS counter, largest
 //       first (LPT).  A team hashes its item's 128-B rows right-aligned to the
-//       group's row count (padded to the ring's 4 rows) through the headline
-//       kernel's row ring: ~init is XORed into the record's first 4 bytes
+//       group's row count (padded to an even count for the two-row ring):
+//       ~init is XORed into the record's first 4 bytes
 //       (identity 3), bytes outside the item are masked, rows before it are
 //       read from a zero block, and crc = ~Z_{-m}(fold), m = ceil128(E) - E.
 //   Records longer than 64 KiB are cut into 64 KiB pieces from their start;

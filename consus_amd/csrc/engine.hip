@@ -147,6 +147,17 @@ int build_device(int device)
                            m ? zeros_op(uint64_t(kRowBytes - m)).then(inv) : Op32::identity());
     }
     {
+        // lane-fold tables: 6-bit slices of the team fold's six shifts (chunk 5 holds bits 30-31)
+        const uint64_t shifts[6] = {16, 12, 8, 4, 32, 64};
+        for (int k = 0; k < 6; ++k)
+        {
+            const Op32 z = zeros_op(shifts[k]);
+            for (int c = 0; c < 6; ++c)
+                for (uint32_t i = 0; i < 64; ++i)
+                    img[kTabLane + (k * 6 + c) * 64 + i] = z.apply(c < 5 ? i << (6 * c) : (i & 3u) << 30);
+        }
+    }
+    {
         // F[n] = Z_n(~0): the register a zero init reaches after n bytes of zeros
         const uint32_t* t0 = &img[kTabT];
         uint32_t f = 0xFFFFFFFFu;
@@ -463,7 +474,7 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     // workgroup puts every item of a small batch into one sorted list)
     int grid = d->cus;
     if (const char* e = std::getenv("MI_CRC32C_SORTED_GRID"))
-        grid = std::max(1, std::min(grid, std::atoi(e)));
+        grid = std::max(1, std::min(8 * grid, std::atoi(e)));
     HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
                           c->stream));
     mi_host::note_sorted_batch();
