@@ -19,6 +19,12 @@ from consus_amd import workload as W  # noqa: E402
 E.init(0)
 R = 1 << 20
 off, ln, total = W.zipf_records(R)
+# ZIPF_DROP_BELOW=n / ZIPF_KEEP_BELOW=n: zero the lengths of the records
+# shorter / not shorter than n bytes (cost of one length class; wrong digest)
+if os.environ.get("ZIPF_DROP_BELOW"):
+    ln = np.where(ln < int(os.environ["ZIPF_DROP_BELOW"]), 0, ln).astype(ln.dtype)
+if os.environ.get("ZIPF_KEEP_BELOW"):
+    ln = np.where(ln < int(os.environ["ZIPF_KEEP_BELOW"]), ln, 0).astype(ln.dtype)
 data = E.DeviceBuffer(total + 16)
 data.fill_splitmix64(W.DATA_SEED)
 d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer(R * 4)
@@ -37,5 +43,5 @@ dig = E.crc32c_device(out, R * 4)
 with open(os.path.join(REPO, "tests", "golden", "digests.json")) as f:
     gold = json.load(f)["zipf_seed0x5eed_data0xda7a5eed_1048576"]["digest"]
 ms = float(np.median(times))
-print(f"{'stream' if PACKED else 'pieces'} zipf median {ms:.4f} ms min {min(times):.4f} -> {total / ms / 1e6:.1f} GB/s "
+print(f"{'stream' if PACKED else 'var'} zipf {int(ln.sum(dtype=np.uint64))} B median {ms:.4f} ms min {min(times):.4f} -> {total / ms / 1e6:.1f} GB/s "
       f"digest {dig:#010x} {'OK' if dig == gold else 'MISMATCH'}")
