@@ -584,6 +584,7 @@ def run_zipf_sharded(args, E, dist, rank, world):
     E.sync()
     dist.barrier()
     E.sync()
+    sorted0 = E.stats().get("sorted_batches", 0)
     t0 = time.perf_counter()
     E.timer_start()
     for _ in range(args.steps):
@@ -592,12 +593,13 @@ def run_zipf_sharded(args, E, dist, rank, world):
     E.sync()
     dist.barrier()
     wall = time.perf_counter() - t0
+    on_sorted = E.stats().get("sorted_batches", 0) - sorted0 == args.steps
     t = torch.tensor([wall, ev], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, ev_max = float(t[0]), float(t[1])
     dig = E.crc32c_device(out, cnt * 4) if cnt else 0
     got = [None] * world
-    dist.all_gather_object(got, (dig, cnt, local_total, ev))
+    dist.all_gather_object(got, (dig, cnt, local_total, ev, on_sorted))
     if rank == 0:
         blocks = golden_digests().get("zipf_seed0x5eed_data0xda7a5eed_blocks", {})
         bd = blocks.get("block_digests", [])
@@ -625,8 +627,9 @@ def run_zipf_sharded(args, E, dist, rank, world):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None,
-                         "kernel": "plan + crc32c_chunk_kernel + finalize (whole step; the "
-                                   "slowest rank's bytes over its own step time)"},
+                         "kernel": ("sorted_cost_kernel + crc32c_sorted_kernel" if all(g[4] for g in got)
+                                    else "plan + crc32c_chunk_kernel + finalize") +
+                                   " (whole step; the slowest rank's bytes over its own step time)"},
             "digest_verified": ok, "digests": [f"{g[0]:#010x}" for g in got],
             "cpu_baseline": None}), flush=True)
     dist.destroy_process_group()

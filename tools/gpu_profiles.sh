@@ -19,10 +19,13 @@ run() {  # name limit cmd...
 stats() {  # config extra-args...
   local c=$1; shift
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_$c" -o k --output-format csv \
-     -- python3 "$ROOT/bench.py" --config "$c" --no-cpu --no-pmc --steps 30 --warmup 5 "$@" > "$OUT/rocprof_$c.log" 2>&1) \
+     -- python3 "$ROOT/bench.py" --config "$c" --no-cpu --no-pmc --sustain-seconds 0 --steps 30 --warmup 5 "$@" > "$OUT/rocprof_$c.log" 2>&1) \
      || { echo "FAILED rocprof $c"; tail -20 "$OUT/rocprof_$c.log"; exit 1; }
   cp "$(find "$OUT/rocprof_$c" -name '*kernel_stats.csv' | head -1)" "$OUT/${c}_kernel_stats.csv"
 }
+if [ "$2" = "stats" ]; then  # only the rocprof legs: tools/gpu_profiles.sh TAG stats CONFIG...
+  shift 2; for c in "$@"; do stats "$c"; done; echo "ALL OK"; exit 0
+fi
 run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench_fixed4k 600 python bench.py
