@@ -2279,7 +2279,19 @@ hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32
 constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
 constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 1;  // rows of the largest item (513)
 constexpr uint32_t kSortBins = kSortRows;                         // bin = kSortRows - rows
-constexpr uint32_t kSortFold = 2;            // cost allowance per item, in rows (fold, masks)
+#ifndef MI_SORT_FOLD
+#define MI_SORT_FOLD 2
+#endif
+// XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
+// and in every timeline measured (tools/sorted_stamps.py, 5 runs on 5 boxes)
+// the odd XCDs finished configs[2] 10-30 us after the even ones with equal
+// shares.  Even workgroups take MI_SORT_XCDW/1000 more cost, odd ones as much
+// less (A/B against equal shares: 0.878-0.905 ms vs 0.885-0.916 at 20;
+// 15 is the default, 0 turns it off).
+#ifndef MI_SORT_XCDW
+#define MI_SORT_XCDW 15
+#endif
+constexpr uint32_t kSortFold = MI_SORT_FOLD;  // cost allowance per item, in rows (fold, masks)
 constexpr uint32_t kSortPer = 1;             // records per thread of a cost block
 constexpr uint32_t kSortRecs = kPlanThreads * kSortPer;
 constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a split record
@@ -2453,6 +2465,17 @@ __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ bl
     uint64_t T[2];
     T[0] = tot / G * b + (tot % G) * b / G;
     T[1] = b + 1 == G ? tot : tot / G * (b + 1) + (tot % G) * (b + 1) / G;
+    if (MI_SORT_XCDW && !(G & 1))
+    {
+        // T(x) = C (1000 x + w (x & 1)) / (1000 G): share 1 + w/1000 for even
+        // b, 1 - w/1000 for odd b; T(G) = C exactly
+        auto at = [&](uint64_t x) {
+            return x >= G ? tot : uint64_t(double(tot) * (double(x) * 1000.0 + MI_SORT_XCDW * double(x & 1)) /
+                                           (double(G) * 1000.0));
+        };
+        T[0] = at(b);
+        T[1] = at(b + 1);
+    }
     if (lane == 0)
         for (int h = 0; h < 2; ++h)
         {
