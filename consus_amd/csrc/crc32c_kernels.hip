@@ -2283,7 +2283,7 @@ constexpr uint32_t kSortBins = kSortRows;                         // bin = kSort
 #define MI_SORT_FOLD 2
 #endif
 // XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
-// and in every timeline measured (tools/sorted_stamps.py, 5 runs on 5 boxes)
+// and in every timeline measured (tools/sorted_stamps.py, 5 GPU sessions)
 // the odd XCDs finished configs[2] 10-30 us after the even ones with equal
 // shares.  Even workgroups take MI_SORT_XCDW/1000 more cost, odd ones as much
 // less (A/B against equal shares: 0.878-0.905 ms vs 0.885-0.916 at 20;
