@@ -19,6 +19,8 @@ E.init(0)
 os.environ["MI_CRC32C_VARPATH"] = "sorted"
 R = 1 << 20
 off, ln, total = W.zipf_records(R)
+if os.environ.get("ZIPF_KEEP_BELOW"):  # one length class only (tools/zipf_probe.py)
+    ln = np.where(ln < int(os.environ["ZIPF_KEEP_BELOW"]), ln, 0).astype(ln.dtype)
 data = E.DeviceBuffer(total + 16)
 data.fill_splitmix64(W.DATA_SEED)
 d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer(R * 4)

@@ -25,6 +25,9 @@ if os.environ.get("ZIPF_DROP_BELOW"):
     ln = np.where(ln < int(os.environ["ZIPF_DROP_BELOW"]), 0, ln).astype(ln.dtype)
 if os.environ.get("ZIPF_KEEP_BELOW"):
     ln = np.where(ln < int(os.environ["ZIPF_KEEP_BELOW"]), ln, 0).astype(ln.dtype)
+# ZIPF_PACK=1: the same records moved back to back (address locality test)
+if os.environ.get("ZIPF_PACK"):
+    off = np.concatenate([[0], np.cumsum(ln[:-1].astype(np.uint64))]).astype(off.dtype) + off[0]
 data = E.DeviceBuffer(total + 16)
 data.fill_splitmix64(W.DATA_SEED)
 d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer(R * 4)
