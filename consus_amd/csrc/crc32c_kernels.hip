@@ -2871,11 +2871,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         return *((g < n_groups && i < n_items) ? (i < n_full ? listF : listL) + i
                                                : reinterpret_cast<const uint4*>(zero16));
     };
-    // Uniform shape of a group: n rows (team 0's item, the largest, padded
-    // to an even count with a leading zero row), the first row of team 0's
-    // item, the last row in which some team's item starts (or its init word
-    // spills into), and the first row from which every lane reads item bytes
-    // (n: never, in a group with teams but no item).
+    // Uniform shape of a group: n rows (its largest item, padded to an even
+    // count with a leading zero row), the first row of that item, the last
+    // row in which some team's item starts (or its init word spills into),
+    // and the first row from which every lane reads item bytes (n: never, in
+    // a group with teams but no item).  The list is descending except where
+    // the 512-row full pieces meet the 513-row whole records (the full
+    // pieces are listed first), so the largest and smallest item are taken
+    // over the group's teams, not from its first and last.
     struct Shape
     {
         int32_t n, fmin, fedge, fast;
@@ -2883,11 +2886,19 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto shape_of = [&](const uint4& d, uint32_t g) {
         Shape s{0, 0, 0, 0};
         if (g >= n_groups) return s;
-        const int32_t rows0 = __builtin_amdgcn_readfirstlane(int(sort_rows(d)));
-        s.n = (rows0 + 1) & ~1;
-        s.fmin = s.n - rows0;
         const uint32_t tlast = min(7u, n_items - 1 - g * 8);
-        s.fedge = s.n - __builtin_amdgcn_readlane(int(sort_rows(d)), int(tlast * kTeam)) + 1;
+        const int rv = int(sort_rows(d));
+        int32_t rmax = 0, rmin = int32_t(kSortRows);
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+        {
+            const int32_t x = __builtin_amdgcn_readlane(rv, int(t * kTeam));
+            rmax = t <= tlast ? max(rmax, x) : rmax;
+            rmin = t <= tlast ? min(rmin, x) : rmin;
+        }
+        s.n = (rmax + 1) & ~1;
+        s.fmin = s.n - rmax;
+        s.fedge = s.n - rmin + 1;
         s.fast = tlast == 7 ? s.fedge + 1 : s.n;
         return s;
     };

@@ -1,7 +1,8 @@
 """Seeded random batches against the oracle (bit-exact), through every
 variable-length entry point: host batches on the direct kernel and on the
 planned path, device batches with and without the size hint, fixed-stride
-batches, and single buffers (host and device).  Shapes mix empty, tiny,
+batches, the sorted path at random grids, and single buffers (host and
+device).  Shapes mix empty, tiny,
 row- and chunk-edge, and multi-chunk records; offsets packed, random,
 overlapping and unordered; inits random or absent.
 
@@ -68,6 +69,22 @@ def test_fuzz_round(engine, oracle, round_):
     for hint in (int(lengths.sum(dtype=np.uint64)), 0):
         engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini, total_bytes=hint)
         assert np.array_equal(d_out.download(np.uint32, count), want), ("device", hint)
+
+    # the sorted path (forced here; the engine takes it by itself from 64 MiB),
+    # one workgroup per CU or a few workgroups (shares cut inside records)
+    grid = [None, "1", "2", "5", "64"][int(rng.integers(0, 5))]
+    os.environ["MI_CRC32C_VARPATH"] = "sorted"
+    if grid:
+        os.environ["MI_CRC32C_SORTED_GRID"] = grid
+    try:
+        before = engine.stats()["sorted_batches"]
+        engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini,
+                            total_bytes=max(int(lengths.sum(dtype=np.uint64)), 1))
+        assert np.array_equal(d_out.download(np.uint32, count), want), ("sorted", grid)
+        assert engine.stats()["sorted_batches"] == before + 1
+    finally:
+        os.environ.pop("MI_CRC32C_VARPATH", None)
+        os.environ.pop("MI_CRC32C_SORTED_GRID", None)
 
     # single buffers: one record on the host and on the device
     i = int(rng.integers(0, count))

@@ -152,6 +152,40 @@ def test_sorted_second_pass(engine, oracle, sorted_path, grid):
         del os.environ["MI_CRC32C_SORTED_GRID"]
 
 
+@pytest.mark.parametrize("grid", ["1", "2", None])
+def test_sorted_513_row_records_beside_512_row_pieces(engine, oracle, sorted_path, grid):
+    """Whole records of 513 rows (<= 64 KiB but straddling 513 windows) in the
+    same workgroup as split records with 128-B-aligned starts, whose full
+    pieces have 512 rows: the full pieces are listed first, so a group can
+    hold a 512-row piece before a 513-row record (found by the fuzz rounds;
+    the group's shape must come from its largest item wherever it sits)."""
+    rng = np.random.default_rng(77)
+    recs = []  # (alignment within 128 B, length)
+    for _ in range(40):
+        recs.append((0, int(rng.integers(65537, 300_000))))     # split, aligned: 512-row pieces
+        recs.append((int(rng.integers(64, 128)), 65536 - int(rng.integers(0, 60))))  # 513 rows
+        recs.append((int(rng.integers(0, 128)), int(rng.integers(4, 9000))))
+    rng.shuffle(recs)
+    offsets, pos = [], 4096
+    for a, L in recs:
+        pos = (pos + 127) // 128 * 128 + a
+        offsets.append(pos)
+        pos += L + int(rng.integers(0, 300))
+    offsets = np.array(offsets, dtype=np.uint64)
+    lengths = np.array([L for _, L in recs], dtype=np.uint32)
+    buf = rng.integers(0, 256, pos + 256, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    if grid:
+        os.environ["MI_CRC32C_SORTED_GRID"] = grid
+    try:
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                              oracle.batch(buf, offsets, lengths, inits))
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                              oracle.batch(buf, offsets, lengths))
+    finally:
+        os.environ.pop("MI_CRC32C_SORTED_GRID", None)
+
+
 def test_sorted_one_huge_record(engine, oracle, sorted_path):
     """One 40 MiB record and a few short ones: the record's 641 pieces are
     spread over many workgroups (the cost split falls inside it)."""
