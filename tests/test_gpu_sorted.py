@@ -267,3 +267,35 @@ def test_sorted_default_for_large_batches(engine, oracle):
     assert np.array_equal(_device_run(engine, buf, offsets, lengths),
                           oracle.batch(buf, offsets, lengths))
     assert engine.stats()["sorted_batches"] == before + 1
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_sorted_fuzz_large(engine, oracle, sorted_path, seed):
+    """Seeded batches of 5K-60K records (at most ~200 MB) through the sorted
+    path at random grids, so that one workgroup's share holds more than 8
+    records per thread (the binning's second pass) as well as fewer; every
+    length class of the GPU fuzz rounds, packed or scattered, with and
+    without inits."""
+    from test_gpu_fuzz import random_lengths
+    rng = np.random.default_rng(5150 + seed)
+    count = int(rng.integers(5_000, 60_000))
+    lengths = np.clip(random_lengths(rng, count), 0, None).astype(np.uint32)
+    while int(lengths.sum(dtype=np.uint64)) > 200 << 20:
+        lengths = (lengths // 2).astype(np.uint32)
+    if rng.integers(0, 2):
+        offsets, end = _packed(rng, lengths, gap=int(rng.integers(0, 9)), start=int(rng.integers(0, 4096)))
+        size = end + 64
+    else:
+        size = int(lengths.max()) + int(rng.integers(1, 64 << 20))
+        offsets = (rng.random(count) * (size - lengths.astype(np.float64))).astype(np.uint64)
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32) if rng.integers(0, 2) else None
+    grid = [None, "1", "2", "3", "16"][int(rng.integers(0, 5))]
+    if grid:
+        os.environ["MI_CRC32C_SORTED_GRID"] = grid
+    try:
+        got = _device_run(engine, buf, offsets, lengths, inits)
+    finally:
+        os.environ.pop("MI_CRC32C_SORTED_GRID", None)
+    assert np.array_equal(got, oracle.batch(buf, offsets, lengths, inits)), grid
+    assert sorted_path() == 1
