@@ -95,7 +95,7 @@ def test_fuzz_round(engine, oracle, round_):
 
     # a fixed-stride batch over the same bytes
     stride = int(rng.integers(1, 5000))
-    flen = int(rng.integers(0, stride + 1))
+    flen = min(int(rng.integers(0, stride + 1)), size)  # the buffer may be shorter
     fcount = max(1, min(500, (size - flen) // stride))
     fini = rng.integers(0, 2**32, fcount, dtype=np.uint32) if rng.integers(0, 2) else None
     assert np.array_equal(engine.crc32c_fixed(buf, stride, flen, fcount, inits=fini),
