@@ -2282,6 +2282,10 @@ constexpr uint32_t kSortBins = kSortRows;                         // bin = kSort
 #ifndef MI_SORT_FOLD
 #define MI_SORT_FOLD 2
 #endif
+// rows per ring of the sorted kernel (2 or 4)
+#ifndef MI_SORT_RING
+#define MI_SORT_RING 2
+#endif
 // XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
 // and in every timeline measured (tools/sorted_stamps.py, 5 GPU sessions)
 // the odd XCDs finished configs[2] 10-30 us after the even ones with equal
@@ -2896,7 +2900,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             rmax = t <= tlast ? max(rmax, x) : rmax;
             rmin = t <= tlast ? min(rmin, x) : rmin;
         }
-        s.n = (rmax + 1) & ~1;
+        s.n = (rmax + MI_SORT_RING - 1) & ~(MI_SORT_RING - 1);
         s.fmin = s.n - rmax;
         s.fedge = s.n - rmin + 1;
         s.fast = tlast == 7 ? s.fedge + 1 : s.n;
@@ -2914,12 +2918,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint4 d_nxt = load_desc(g_nxt);
     Shape sh = shape_of(d_cur, g_cur);
     SortView cur = sort_view(d_cur, sh.n, tl, inits, zero_word, ones_word);
-    // Two-row ring: even rows in b0, odd rows in b1; each row step issues the
-    // next row (this group's, or row 0 of the next group) before folding the
-    // current one.  Groups have an even row count, so the roles never change.
-    // (Measured on the headline batch: one row ahead costs < 1 % against
-    // three; here it keeps the padding to half a row per group.)
-    uint4 b0 = load16(row_ptr(cur, 0, false)), b1;
+    // Row ring of RB buffers: row r of a group sits in b[r % RB]; each row
+    // step issues row r + RB - 1 (this group's, or one of the next group's
+    // first rows) before folding row r.  Groups are padded to a multiple of
+    // RB rows, so the roles never change.  RB = 2 (MI_SORT_RING): one row in
+    // flight per wave while another folds (measured on the headline batch:
+    // one row ahead costs < 1 % against three; here it keeps the padding to
+    // half a row per group).
+    constexpr int RB = MI_SORT_RING;
+    uint4 b[RB];
+#pragma unroll
+    for (int j = 0; j < RB - 1; ++j) b[j] = load16(row_ptr(cur, j, false));
     __builtin_amdgcn_sched_barrier(0);
     while (sh.n > 0)
     {
@@ -2931,7 +2940,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
         // General row: padding skip, start mask and init word (rows up to
         // fedge), end mask (row n - 1), zero-block reads.  Used for the first
-        // rows and the last two of a group; the rows between take the body
+        // rows and the last RB of a group; the rows between take the body
         // loop below: all lanes read item bytes, nothing to mask.
         auto gen_row = [&](uint4 d, int32_t r) {
             if (r < fmin) return;  // the padding row: V stays 0
@@ -2954,41 +2963,45 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                 d.w &= cur.ke.w;
             }
             if (r == fmin)
-                row_first(V, d);  // team 0 starts here; every other team's row is zero
+                row_first(V, d);  // the largest item starts here; every other team's row is zero
             else
                 row_update(V, d, li);
         };
-        // body rows [hend, n - 2): after every team's first row and init
+        // body rows [hend, n - RB): after every team's first row and init
         // word (full groups only: a partial group has teams without items)
-        const int32_t hend = fast < n ? min(n - 2, (fedge + 2) & ~1) : n - 2;
+        const int32_t hend = fast < n ? min(n - RB, (fedge + RB) & ~(RB - 1)) : n - RB;
         int32_t r = 0;
-        for (; r < hend; r += 2)
+        for (; r < hend; r += RB)
         {
-            b1 = load16(row_ptr(cur, r + 1, false));
-            __builtin_amdgcn_sched_barrier(0);
-            gen_row(b0, r);
-            b0 = load16(row_ptr(cur, r + 2, false));
-            __builtin_amdgcn_sched_barrier(0);
-            gen_row(b1, r + 1);
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+            {
+                b[(j + RB - 1) % RB] = load16(row_ptr(cur, r + j + RB - 1, false));
+                __builtin_amdgcn_sched_barrier(0);
+                gen_row(b[j], r + j);
+            }
         }
         {
             const uint8_t* pr = reinterpret_cast<const uint8_t*>(cur.p0);
-            for (; r < n - 2; r += 2)
+            for (; r < n - RB; r += RB)
             {
-                b1 = load16(pr + uint32_t(r + 1) * uint32_t(kRowBytes));
-                __builtin_amdgcn_sched_barrier(0);
-                row_update(V, b0, li);
-                b0 = load16(pr + uint32_t(r + 2) * uint32_t(kRowBytes));
-                __builtin_amdgcn_sched_barrier(0);
-                row_update(V, b1, li);
+#pragma unroll
+                for (int j = 0; j < RB; ++j)
+                {
+                    b[(j + RB - 1) % RB] = load16(pr + uint32_t(r + j + RB - 1) * uint32_t(kRowBytes));
+                    __builtin_amdgcn_sched_barrier(0);
+                    row_update(V, b[j], li);
+                }
             }
         }
-        b1 = load16(row_ptr(cur, n - 1, false));
-        __builtin_amdgcn_sched_barrier(0);
-        gen_row(b0, n - 2);
-        b0 = load16(row_ptr(nxt, 0, false));
-        __builtin_amdgcn_sched_barrier(0);
-        gen_row(b1, n - 1);
+        // the last RB rows: row n - 1, then the next group's first rows
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+        {
+            b[(j + RB - 1) % RB] = load16(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
+            __builtin_amdgcn_sched_barrier(0);
+            gen_row(b[j], n - RB + j);
+        }
         const uint32_t W = team_fold(V);
         flush();  // the previous group's items
         {
