@@ -1,8 +1,8 @@
 """Seeded random batches against the oracle (bit-exact), through every
 variable-length entry point: host batches on the direct kernel and on the
 planned path, device batches with and without the size hint, fixed-stride
-batches, the sorted path at random grids, and single buffers (host and
-device).  Shapes mix empty, tiny,
+batches, the sorted path at random grids, the opt-in stream path, and
+single buffers (host and device).  Shapes mix empty, tiny,
 row- and chunk-edge, and multi-chunk records; offsets packed, random,
 overlapping and unordered; inits random or absent.
 
@@ -85,6 +85,13 @@ def test_fuzz_round(engine, oracle, round_):
     finally:
         os.environ.pop("MI_CRC32C_VARPATH", None)
         os.environ.pop("MI_CRC32C_SORTED_GRID", None)
+
+    # the opt-in stream path (MI_CRC32C_PACKED): records in address order are
+    # hashed as one stream; any other order takes its exact byte-serial
+    # fallback, so both layouts must match
+    engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini,
+                        total_bytes=int(lengths.sum(dtype=np.uint64)), packed=True)
+    assert np.array_equal(d_out.download(np.uint32, count), want), ("stream", layout)
 
     # single buffers: one record on the host and on the device
     i = int(rng.integers(0, count))
