@@ -1,7 +1,8 @@
 """Seeded random batches against the oracle (bit-exact), through every
 variable-length entry point: host batches on the direct kernel and on the
 planned path, device batches with and without the size hint, fixed-stride
-batches, the sorted path at random grids, the opt-in stream path, and
+batches (also split over 2-5 ranges through the multi-device entry
+points), the sorted path at random grids, the opt-in stream path, and
 single buffers (host and device).  Shapes mix empty, tiny,
 row- and chunk-edge, and multi-chunk records; offsets packed, random,
 overlapping and unordered; inits random or absent.
@@ -54,6 +55,10 @@ def test_fuzz_round(engine, oracle, round_):
     for planned in (False, True):
         got = engine.crc32c_batch(buf, offsets, lengths, inits, planned=planned)
         assert np.array_equal(got, want), ("host", planned)
+    # the multi-device entry point, split into 2-5 byte-balanced ranges on the one GPU
+    ndev = int(rng.integers(2, 6))
+    got = engine.crc32c_batch_multi(buf, offsets, lengths, inits, devices=[0] * ndev, shard_min=1)
+    assert np.array_equal(got, want), ("multi", ndev)
 
     # device batch, with the size hint and without it (plan read-back)
     data = engine.DeviceBuffer(size)
@@ -105,7 +110,9 @@ def test_fuzz_round(engine, oracle, round_):
     flen = min(int(rng.integers(0, stride + 1)), size)  # the buffer may be shorter
     fcount = max(1, min(500, (size - flen) // stride))
     fini = rng.integers(0, 2**32, fcount, dtype=np.uint32) if rng.integers(0, 2) else None
-    assert np.array_equal(engine.crc32c_fixed(buf, stride, flen, fcount, inits=fini),
-                          oracle.fixed(buf, stride, flen, fcount, inits=fini)), (stride, flen)
+    fwant = oracle.fixed(buf, stride, flen, fcount, inits=fini)
+    assert np.array_equal(engine.crc32c_fixed(buf, stride, flen, fcount, inits=fini), fwant), (stride, flen)
+    assert np.array_equal(engine.crc32c_fixed_multi(buf, stride, flen, fcount, inits=fini,
+                                                    devices=[0] * ndev, shard_min=1), fwant), ("fixed multi", ndev)
     for b in (data, d_off, d_len, d_out) + ((d_ini,) if d_ini is not None else ()):
         b.free()
