@@ -2303,7 +2303,8 @@ constexpr uint32_t kSortFirst = 0x40000000u;  // ... its first piece (carries th
 constexpr uint32_t kSortRecMask = 0x3FFFFFFFu;
 constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
 
-// measurement builds only: MI_SORT_STAMP=1 records s_memrealtime stamps
+// measurement builds only: MI_SORT_STAMP=1 (2: slots 6 and 7 = the wave's
+// first group of <= 8 and of <= 2 rows) records s_memrealtime stamps
 // (100 MHz) per wave into the item workspace past item_cap, 8 words: start,
 // end of the prologue, end of the last group, then after the table staging,
 // the block search, the boundaries, binning pass 1 and the item allocation
@@ -2660,7 +2661,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t* const stamps = reinterpret_cast<uint64_t*>(items + item_cap) +
                              (uint64_t(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64) * 8;
-    if (MI_SORT_STAMP && lane == 0) stamps[0] = __builtin_amdgcn_s_memrealtime();
+    if (MI_SORT_STAMP && lane == 0)
+    {
+        stamps[0] = __builtin_amdgcn_s_memrealtime();
+        stamps[6] = 0;
+        stamps[7] = 0;
+    }
     if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = 0;
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
@@ -2772,7 +2778,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     pass(false);
     __syncthreads();
-    if (MI_SORT_STAMP && lane == 0) stamps[6] = __builtin_amdgcn_s_memrealtime();
+    if (MI_SORT_STAMP == 1 && lane == 0) stamps[6] = __builtin_amdgcn_s_memrealtime();
     {
         const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
         uint64_t total;
@@ -2800,7 +2806,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         }
     }
     __syncthreads();
-    if (MI_SORT_STAMP && lane == 0) stamps[7] = __builtin_amdgcn_s_memrealtime();
+    if (MI_SORT_STAMP == 1 && lane == 0) stamps[7] = __builtin_amdgcn_s_memrealtime();
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     if (n_items)
     {
@@ -2938,6 +2944,13 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const SortView nxt = sort_view(d_nxt, shn.n, tl, inits, zero_word, ones_word);
         uint32_t V[4] = {0, 0, 0, 0};
         const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
+        if (MI_SORT_STAMP == 2 && lane == 0)
+        {
+            // the wave's first group of <= 8 rows (slot 6) and of <= 2 rows (slot 7)
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (n <= 8 && stamps[6] == 0) stamps[6] = now;
+            if (n <= 2 && stamps[7] == 0) stamps[7] = now;
+        }
         // General row: padding skip, start mask and init word (rows up to
         // fedge), end mask (row n - 1), zero-block reads.  Used for the first
         // rows and the last RB of a group; the rows between take the body

@@ -39,8 +39,12 @@ pro = (st[:, 1] - t0) / 100.0
 end = (st[:, 2] - t0) / 100.0
 q = lambda a: " ".join(f"{p}%={np.percentile(a, p):.1f}" for p in (0, 1, 10, 50, 90, 99, 100))
 print("start   ", q((st[:, 0] - t0) / 100.0))
-for i, name in ((3, "staged"), (4, "blocks found"), (5, "resolved"), (6, "pass 1"), (7, "allocated"), (1, "pass 2 = prologue")):
-    print(f"{name:18s}", q((st[:, i] - t0) / 100.0))
+MODE2 = os.environ.get("STAMP_MODE") == "2"  # a MI_SORT_STAMP=2 build
+for i, name in ((3, "staged"), (4, "blocks found"), (5, "resolved"),
+                (6, "first <= 8 rows" if MODE2 else "pass 1"), (7, "first <= 2 rows" if MODE2 else "allocated"),
+                (1, "pass 2 = prologue")):
+    v = st[:, i][st[:, i] > 0] if MODE2 and i in (6, 7) else st[:, i]
+    print(f"{name:18s}", q((v - t0) / 100.0), f"({v.size} waves)" if MODE2 and i in (6, 7) else "")
 print("end     ", q(end))
 wg_end = end.reshape(256, 16).max(axis=1)
 wg_min = end.reshape(256, 16).min(axis=1)
