@@ -1,6 +1,5 @@
+#!/bin/bash
+# A/B of sorted-path library builds on configs[2] (dev tool):
+#   tools/build_variant.sh TAG -DMI_SORT_...=... ; tools/sorted_knobs.sh tools/ab/libconsus_crc32c_TAG.so ...
 set -o pipefail
-mkdir -p gpurun_out/lay
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/lay/gpu.txt 2>&1 || { tail -30 gpurun_out/lay/gpu.txt; exit 1; }
-tail -1 gpurun_out/lay/gpu.txt
-AB_ROUNDS=5 timeout -k 10 900 python tools/ab.py --zipf tools/ab/libconsus_crc32c_lold.so tools/ab/libconsus_crc32c_lnew.so
-AB_ROUNDS=5 timeout -k 10 900 python tools/ab.py tools/ab/libconsus_crc32c_lold.so tools/ab/libconsus_crc32c_lnew.so
+AB_ROUNDS=${AB_ROUNDS:-4} timeout -k 10 900 python tools/ab.py --zipf "$@"
