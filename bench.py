@@ -67,7 +67,11 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps before the K timed ones (default 300 for the "
+                         "device-resident configs -- about 0.2 s, the clock ramp: with 5 the "
+                         "timed launches ran 1-2.5 %% below the sustained rate -- and 5 for "
+                         "stream/pcie4k/dlog)")
     ap.add_argument("--sustain-seconds", type=float, default=3.0,
                     help="fixed4k: after the timed region, launch back to back for this long and "
                          "report the sustained per-GPU rate (clock/power droop check; 0 = off)")
@@ -98,7 +102,10 @@ def parse():
                     help="N>1: skip the RCCL all-gather of the CRC vectors after the timed region")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank uses device 0 (no RCCL gather)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.warmup is None:
+        args.warmup = 300 if args.config in ("fixed4k", "zipf", "single") else 5
+    return args
 
 
 def golden_digests():
