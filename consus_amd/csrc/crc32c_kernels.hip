@@ -2286,6 +2286,10 @@ constexpr uint32_t kSortBins = kSortRows;                         // bin = kSort
 #ifndef MI_SORT_RING
 #define MI_SORT_RING 2
 #endif
+// group loop unrolled twice with the current/next views swapped (no copies)
+#ifndef MI_SORT_PINGPONG
+#define MI_SORT_PINGPONG 1
+#endif
 // XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
 // and in every timeline measured (tools/sorted_stamps.py, 5 GPU sessions)
 // the odd XCDs finished configs[2] 10-30 us after the even ones with equal
@@ -2607,12 +2611,48 @@ __device__ __forceinline__ uint32_t init_dword(uint32_t ninit, int32_t q, int k)
 
 // The masks depend on the record's init, loaded here and consumed a group
 // later (sort_view runs for the NEXT group), so the load costs no wait.
+#ifndef MI_SORT_VIEW32
+#define MI_SORT_VIEW32 1
+#endif
 __device__ __forceinline__ SortView sort_view(const uint4& d, int32_t n, uint32_t tl,
                                               const uint32_t* __restrict__ inits,
                                               const uint32_t* __restrict__ zero_word,
                                               const uint32_t* __restrict__ ones_word)
 {
     SortView v;
+#if MI_SORT_VIEW32
+    // 32-bit window arithmetic (an item spans < 2^17 bytes); one 64-bit add
+    // for the row pointer.  The init word: (hi:lo) = ~init << 8 (q & 3) goes
+    // to dwords q>>2 and q>>2 + 1 of the lane's block (q = the record's
+    // first byte there, -3..15), or to row f + 1 (lane 0, q >= 125).
+    {
+        const uint32_t L = d.z;
+        const int32_t s0 = int32_t(d.x & (kRowBytes - 1));
+        const int32_t se = s0 + int32_t(L);
+        const int32_t rows = L ? (se + int32_t(kRowBytes) - 1) >> 7 : 0;
+        v.recf = L ? d.w : kSortNone;
+        v.f = n - rows;
+        const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
+        v.p0 = ps + int64_t(int32_t(uint32_t(rows - n) * kRowBytes + tl * 16u) - s0);
+        const int32_t q = s0 - int32_t(tl) * 16;
+        const int32_t bs = min(max(q, 0), 16);
+        const int32_t ce = min(max(se - (rows - 1) * int32_t(kRowBytes) - int32_t(tl) * 16, 0), 16);
+        v.lo = L ? v.f + (bs >= 16 ? 1 : 0) : n;
+        v.hi = L ? n - 1 - (ce == 0 ? 1 : 0) : -1;
+        v.m = uint32_t(rows * int32_t(kRowBytes) - se);
+        v.kf = make_uint4(keep_from(bs, 0), keep_from(bs, 1), keep_from(bs, 2), keep_from(bs, 3));
+        v.ke = make_uint4(keep_below(ce, 0), keep_below(ce, 1), keep_below(ce, 2), keep_below(ce, 3));
+        const bool with_init = L && (!(d.w & kSortMulti) || (d.w & kSortFirst));
+        const uint32_t ninit = ~*(!with_init ? ones_word : inits ? inits + (d.w & kSortRecMask) : zero_word);
+        const uint64_t sh = uint64_t(ninit) << ((uint32_t(q) & 3u) * 8u);
+        const uint32_t xl = uint32_t(sh), xh = uint32_t(sh >> 32);
+        const int32_t qd = q >> 2;  // arithmetic: -1 for q in -3..-1
+        v.xf = make_uint4(qd == 0 ? xl : qd == -1 ? xh : 0u, qd == 1 ? xl : qd == 0 ? xh : 0u,
+                          qd == 2 ? xl : qd == 1 ? xh : 0u, qd == 3 ? xl : qd == 2 ? xh : 0u);
+        v.xs = q >= int32_t(kRowBytes) - 3 ? xh : 0u;
+        return v;
+    }
+#endif
     const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
     const uint64_t E = ps + d.z;
     const uint64_t w0 = ps & ~uint64_t(kRowBytes - 1), w1 = (E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
@@ -2922,8 +2962,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint4 d_cur = load_desc(g_cur);
     uint32_t g_nxt = grab();
     uint4 d_nxt = load_desc(g_nxt);
-    Shape sh = shape_of(d_cur, g_cur);
-    SortView cur = sort_view(d_cur, sh.n, tl, inits, zero_word, ones_word);
+    Shape shA = shape_of(d_cur, g_cur);
+    SortView vA = sort_view(d_cur, shA.n, tl, inits, zero_word, ones_word);
+    Shape shB{0, 0, 0, 0};
+    SortView vB = vA;
+    const SortView& cur0 = vA;
     // Row ring of RB buffers: row r of a group sits in b[r % RB]; each row
     // step issues row r + RB - 1 (this group's, or one of the next group's
     // first rows) before folding row r.  Groups are padded to a multiple of
@@ -2934,14 +2977,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     constexpr int RB = MI_SORT_RING;
     uint4 b[RB];
 #pragma unroll
-    for (int j = 0; j < RB - 1; ++j) b[j] = load16(row_ptr(cur, j, false));
+    for (int j = 0; j < RB - 1; ++j) b[j] = load16(row_ptr(cur0, j, false));
     __builtin_amdgcn_sched_barrier(0);
-    while (sh.n > 0)
-    {
+    // One group: hash `cur` (shape sh) while the next group's view is built
+    // into `nxt`.  The loop runs it twice per iteration with the two views
+    // swapped (MI_SORT_PINGPONG), so the ~20 registers of a view are never
+    // copied at the back edge.
+    auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
         const uint32_t g_nn = grab();
         const uint4 d_nn = load_desc(g_nn);
-        const Shape shn = shape_of(d_nxt, g_nxt);
-        const SortView nxt = sort_view(d_nxt, shn.n, tl, inits, zero_word, ones_word);
+        shn = shape_of(d_nxt, g_nxt);
+        nxt = sort_view(d_nxt, shn.n, tl, inits, zero_word, ones_word);
         uint32_t V[4] = {0, 0, 0, 0};
         const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
         if (MI_SORT_STAMP == 2 && lane == 0)
@@ -3029,12 +3075,24 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             p_recf = cur.recf;
             p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;  // lane 0: the item's end
         }
-        g_cur = g_nxt;
-        cur = nxt;
-        sh = shn;
         g_nxt = g_nn;
         d_nxt = d_nn;
+    };
+#if MI_SORT_PINGPONG
+    while (shA.n > 0)
+    {
+        step(vA, shA, vB, shB);
+        if (shB.n <= 0) break;
+        step(vB, shB, vA, shA);
     }
+#else
+    while (shA.n > 0)
+    {
+        step(vA, shA, vB, shB);
+        vA = vB;
+        shA = shB;
+    }
+#endif
     flush();
     if (MI_SORT_STAMP && lane == 0) stamps[2] = __builtin_amdgcn_s_memrealtime();
 }
