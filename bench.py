@@ -72,9 +72,10 @@ def parse():
                          "device-resident configs -- about 0.2 s, the clock ramp: with 5 the "
                          "timed launches ran 1-2.5 %% below the sustained rate -- and 5 for "
                          "stream/pcie4k/dlog)")
-    ap.add_argument("--sustain-seconds", type=float, default=3.0,
+    ap.add_argument("--sustain-seconds", type=float, default=8.0,
                     help="fixed4k: after the timed region, launch back to back for this long and "
-                         "report the sustained per-GPU rate (clock/power droop check; 0 = off)")
+                         "report the sustained per-GPU rate (clock/power droop check; it also keeps "
+                         "the GPU busy long enough for an external utilisation sampler; 0 = off)")
     ap.add_argument("--config", default="fixed4k",
                     choices=["fixed4k", "zipf", "stream", "pcie4k", "single", "dlog"],
                     help="fixed4k = BASELINE configs[1] (headline, default); zipf = configs[2] "
