@@ -2301,6 +2301,13 @@ constexpr uint32_t kSortBins = kSortRows;                         // bin = kSort
 #ifndef MI_SORT_RING
 #define MI_SORT_RING 2
 #endif
+// measurement knob: groups grabbed from a per-workgroup counter in global
+// memory (256-B spaced, zeroed by sorted_cost_kernel) instead of LDS: the
+// owner-side cost of any cross-workgroup stealing scheme
+#ifndef MI_SORT_GGRAB
+#define MI_SORT_GGRAB 0
+#endif
+constexpr uint32_t kSortWgcBase = 64, kSortWgcStride = 64;  // ctrl words
 // group loop unrolled twice with the current/next views swapped (no copies)
 #ifndef MI_SORT_PINGPONG
 #define MI_SORT_PINGPONG 1
@@ -2373,7 +2380,7 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     uint64_t* __restrict__ blk_cost, uint32_t* __restrict__ ctrl, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables)
+    const uint32_t* __restrict__ tables, uint32_t nwg)
 {
     __shared__ uint64_t sh[kPlanThreads / 64];
     const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kSortPer;
@@ -2410,6 +2417,10 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
             ctrl[1] = 0;  // overflow flag
         }
     }
+    if (MI_SORT_GGRAB)
+        for (uint64_t w = uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x; w < nwg;
+             w += uint64_t(gridDim.x) * kPlanThreads)
+            ctrl[kSortWgcBase + w * kSortWgcStride] = 0;
 }
 
 // LDS of the sorted kernel beyond the table image.
@@ -2926,7 +2937,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     auto grab = [&]() {
         uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(&S.next_group, 1u);
+        if (MI_SORT_GGRAB)
+        {
+            if (lane == 0)
+                g = __hip_atomic_fetch_add(ctrl + kSortWgcBase + uint64_t(blockIdx.x) * kSortWgcStride,
+                                           1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        else if (lane == 0)
+            g = atomicAdd(&S.next_group, 1u);
         return uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
     };
     const uint4* const listF = items + count + S.full_base;  // full pieces first
@@ -3121,7 +3139,7 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     const uint32_t nb = sorted_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
     hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
-                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables);
+                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, uint32_t(grid));
     hipLaunchKernelGGL(crc32c_sorted_kernel, dim3(grid), dim3(kBlock), kLdsSorted, stream, b,
                        offsets, lengths, inits, count, ws.blk_cost, nb, ws.ctrl, ws.items,
                        ws.item_cap, out, tables, pow2);

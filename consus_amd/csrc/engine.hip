@@ -463,9 +463,10 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
 {
     const uint64_t cap = sorted_item_cap(count, total_bytes);
     int st;
-    // + a stamp area for MI_SORT_STAMP measurement builds (8 words per wave)
+    // + a stamp area for MI_SORT_STAMP measurement builds (8 words per wave);
+    // ctrl: 64 words, then one 256-B slot per workgroup (MI_SORT_GGRAB builds)
     if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
-        (st = c->srt_ctrl.reserve(16)) || (st = c->srt_items.reserve(cap * 16 + 65536 * 64)))
+        (st = c->srt_ctrl.reserve(4 * (64 + 64 * uint64_t(8 * d->cus)))) || (st = c->srt_items.reserve(cap * 16 + 65536 * 64)))
         return st;
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        c->srt_items.as<uint4>(), (c->srt_items.cap - 65536 * 64) / 16};
