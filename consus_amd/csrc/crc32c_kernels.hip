@@ -2376,46 +2376,67 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
     return uint64_t(lo) | (uint64_t(hi) << 32);
 }
 
+// Cost blocks per launch block (MI_SORT_COSTX): thread t of block j takes
+// record t of cost blocks X j .. X j + X - 1, all loads issued first.
+#ifndef MI_SORT_COSTX
+#define MI_SORT_COSTX 1
+#endif
 __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     uint64_t* __restrict__ blk_cost, uint32_t* __restrict__ ctrl, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, uint32_t nwg)
 {
-    __shared__ uint64_t sh[kPlanThreads / 64];
-    const uint64_t r0 = (uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x) * kSortPer;
-    uint64_t c = 0;
+    static_assert(kSortPer == 1, "one record per thread and cost block");
+    constexpr uint32_t X = MI_SORT_COSTX;
+    __shared__ uint64_t sh[X][kPlanThreads / 64];
+    uint64_t av[X];
+    uint32_t Lv[X];
 #pragma unroll
-    for (uint32_t q = 0; q < kSortPer; ++q)
+    for (uint32_t x = 0; x < X; ++x)
     {
-        const uint64_t r = r0 + q;
-        if (r >= count) break;
-        const uint8_t* p = base + off[r];
-        const uint32_t L = len[r];
-        if (L < 4)
-        {
-            uint32_t x = ~(inits ? inits[r] : 0u);
-            for (uint32_t i = 0; i < L; ++i) x = tables[kTabT + ((x ^ p[i]) & 0xFFu)] ^ (x >> 8);
-            out[r] = ~x;
-            continue;
-        }
-        const SortCost s = sort_cost(uint64_t(p), L);
-        c += s.cost;
-        if (s.n > 1) out[r] = ~0u;  // the pieces XOR their parts in
+        const uint64_t r = (uint64_t(blockIdx.x) * X + x) * kPlanThreads + threadIdx.x;
+        av[x] = r < count ? off[r] : 0;
+        Lv[x] = r < count ? len[r] : 4u;  // past the end: no cost, no store
     }
-    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
-    if ((threadIdx.x & 63u) == 0) sh[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0)
+#pragma unroll
+    for (uint32_t x = 0; x < X; ++x)
     {
-        uint64_t t = 0;
-        for (uint32_t w = 0; w < kPlanThreads / 64; ++w) t += sh[w];
-        blk_cost[blockIdx.x] = t;
-        if (blockIdx.x == 0)
+        const uint64_t r = (uint64_t(blockIdx.x) * X + x) * kPlanThreads + threadIdx.x;
+        uint64_t c = 0;
+        if (r < count)
         {
-            ctrl[0] = 0;  // item allocation cursor
-            ctrl[1] = 0;  // overflow flag
+            const uint8_t* p = base + av[x];
+            const uint32_t L = Lv[x];
+            if (L < 4)
+            {
+                uint32_t h = ~(inits ? inits[r] : 0u);
+                for (uint32_t i = 0; i < L; ++i) h = tables[kTabT + ((h ^ p[i]) & 0xFFu)] ^ (h >> 8);
+                out[r] = ~h;
+            }
+            else
+            {
+                const SortCost sc = sort_cost(uint64_t(p), L);
+                c = sc.cost;
+                if (sc.n > 1) out[r] = ~0u;  // the pieces XOR their parts in
+            }
         }
+        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+        if ((threadIdx.x & 63u) == 0) sh[x][threadIdx.x >> 6] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < X)
+    {
+        const uint32_t x = threadIdx.x;
+        uint64_t t = 0;
+        for (uint32_t w = 0; w < kPlanThreads / 64; ++w) t += sh[x][w];
+        const uint64_t cb = uint64_t(blockIdx.x) * X + x;
+        if (cb * kPlanThreads < count) blk_cost[cb] = t;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+    {
+        ctrl[0] = 0;  // item allocation cursor
+        ctrl[1] = 0;  // overflow flag
     }
     if (MI_SORT_GGRAB)
         for (uint64_t w = uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x; w < nwg;
@@ -3138,7 +3159,8 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     if (count == 0) return hipSuccess;
     const uint32_t nb = sorted_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
-    hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
+    hipLaunchKernelGGL(sorted_cost_kernel, dim3((nb + MI_SORT_COSTX - 1) / MI_SORT_COSTX),
+                       dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, uint32_t(grid));
     hipLaunchKernelGGL(crc32c_sorted_kernel, dim3(grid), dim3(kBlock), kLdsSorted, stream, b,
                        offsets, lengths, inits, count, ws.blk_cost, nb, ws.ctrl, ws.items,
