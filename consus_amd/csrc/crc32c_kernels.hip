@@ -2308,6 +2308,10 @@ constexpr uint32_t kSortBins = kSortRows;                         // bin = kSort
 #define MI_SORT_GGRAB 0
 #endif
 constexpr uint32_t kSortWgcBase = 64, kSortWgcStride = 64;  // ctrl words
+// 2-row groups: the last row issued at the group's start (see step)
+#ifndef MI_SORT_SHORTPRE
+#define MI_SORT_SHORTPRE 1
+#endif
 // group loop unrolled twice with the current/next views swapped (no copies)
 #ifndef MI_SORT_PINGPONG
 #define MI_SORT_PINGPONG 1
@@ -3038,6 +3042,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // swapped (MI_SORT_PINGPONG), so the ~20 registers of a view are never
     // copied at the back edge.
     auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
+        // A 2-row group runs no body loop, so its last row can be issued now,
+        // a whole group header ahead of its folding, instead of one row
+        // ahead (MI_SORT_SHORTPRE); b[1] is free here.
+        const bool pre = MI_SORT_SHORTPRE && RB == 2 && sh.n == 2;
+        if (pre) b[1] = load16(row_ptr(cur, 1, false));
         const uint32_t g_nn = grab();
         const uint4 d_nn = load_desc(g_nn);
         shn = shape_of(d_nxt, g_nxt);
@@ -3111,7 +3120,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 #pragma unroll
         for (int j = 0; j < RB; ++j)
         {
-            b[(j + RB - 1) % RB] = load16(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
+            if (!(j == 0 && pre))
+                b[(j + RB - 1) % RB] = load16(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
             __builtin_amdgcn_sched_barrier(0);
             gen_row(b[j], n - RB + j);
         }
