@@ -2342,9 +2342,10 @@ constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
 #ifndef MI_SORT_STAMP
 #define MI_SORT_STAMP 0
 #endif
-// measurement builds only (tools/build_variant.sh), results are wrong: stop
-// after the binning (1), the block search (2), the boundaries (3), the
-// table staging (4): times the prologue's phases
+// measurement builds only (tools/build_variant.sh, tools/stop_probe.sh),
+// results are wrong: stop after the descriptors (1), the block search (2),
+// the boundaries (3), the table staging (4), binning pass 1 (5), the bin
+// scan and item allocation (6): times the prologue's phases
 #ifndef MI_SORT_STOP
 #define MI_SORT_STOP 0
 #endif
@@ -2870,6 +2871,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     pass(false);
     __syncthreads();
     if (MI_SORT_STAMP == 1 && lane == 0) stamps[6] = __builtin_amdgcn_s_memrealtime();
+    if (MI_SORT_STOP == 5) return;
     {
         const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
         uint64_t total;
@@ -2898,6 +2900,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     __syncthreads();
     if (MI_SORT_STAMP == 1 && lane == 0) stamps[7] = __builtin_amdgcn_s_memrealtime();
+    if (MI_SORT_STOP == 6) return;
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     if (n_items)
     {
