@@ -66,7 +66,10 @@ KERNEL_MATCH = "crc32c_fixed"             # PMC rows: either fixed-length kernel
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 200 for the device-resident configs -- a "
+                         "0.13-0.17 s timed region, so a short clock or power transient moves "
+                         "the line by a fraction of a percent; 50 for stream/pcie4k/dlog)")
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed steps before the K timed ones (default 300 for the "
                          "device-resident configs -- about 0.2 s, the clock ramp: with 5 the "
@@ -106,6 +109,8 @@ def parse():
     args = ap.parse_args()
     if args.warmup is None:
         args.warmup = 300 if args.config in ("fixed4k", "zipf", "single") else 5
+    if args.steps is None:
+        args.steps = 200 if args.config in ("fixed4k", "zipf", "single") else 50
     return args
 
 
