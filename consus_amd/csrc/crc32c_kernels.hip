@@ -2314,6 +2314,10 @@ constexpr uint32_t kSortBins = kSortRows;                         // bin = kSort
 #define MI_SORT_GGRAB 0
 #endif
 constexpr uint32_t kSortWgcBase = 64, kSortWgcStride = 64;  // ctrl words
+// measurement knob: descriptors read with non-temporal loads
+#ifndef MI_SORT_NTDLOAD
+#define MI_SORT_NTDLOAD 0
+#endif
 // measurement knob: the CRCs written with non-temporal stores
 #ifndef MI_SORT_NTOUT
 #define MI_SORT_NTOUT 0
@@ -3008,8 +3012,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint4* const listL = items + rlo - n_full;          // then the rest
     auto load_desc = [&](uint32_t g) {
         const uint32_t i = g * 8 + tw;
-        return *((g < n_groups && i < n_items) ? (i < n_full ? listF : listL) + i
-                                               : reinterpret_cast<const uint4*>(zero16));
+        const uint4* p = (g < n_groups && i < n_items) ? (i < n_full ? listF : listL) + i
+                                                       : reinterpret_cast<const uint4*>(zero16);
+        // MI_SORT_NTDLOAD: read once, so a non-temporal load
+        return MI_SORT_NTDLOAD ? load16(reinterpret_cast<const uint8_t*>(p)) : *p;
     };
     // Uniform shape of a group: n rows (its largest item, padded to an even
     // count with a leading zero row), the first row of that item, the last
