@@ -101,6 +101,15 @@ def parse():
                     help="wall budget of each CPU-baseline leg (single, all-threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="fixed4k at N = 1: skip the other single-GPU BASELINE configs that the "
+                         "headline line carries by default (configs[2] zipf, configs[4] stream, "
+                         "the PCIe-inclusive configs[1] rate)")
+    ap.add_argument("--leg-sustain-seconds", type=float, default=2.0,
+                    help="zipf: back-to-back steps after the timed region for this long (0 = off)")
+    ap.add_argument("--leg-cpu-seconds", type=float, default=3.0,
+                    help="zipf/stream/pcie4k: wall budget of the reference-CPU leg on the same "
+                         "bytes")
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the RCCL all-gather of the CRC vectors after the timed region")
@@ -127,7 +136,9 @@ def pmc_traffic(args) -> tuple[float | None, str]:
     """Run this script under `rocprofv3 --pmc FETCH_SIZE` (its own pass, no
     tracing domains) and return corrected HBM read bytes per launch of the
     fixed kernel (fixed4k) or per step of the variable path (zipf: every
-    plan, chunk and finalize dispatch of one step)."""
+    cost/hash (sorted path) or plan, chunk and finalize (piece path)
+    dispatch of one step; stream/pcie4k: every CRC kernel of one step's
+    segments -- the H2D/D2H copies are DMA, not kernels)."""
     exe = shutil.which("rocprofv3")
     if not exe:
         return None, "rocprofv3 not found"
@@ -144,7 +155,8 @@ def pmc_traffic(args) -> tuple[float | None, str]:
         return None, f"rocprofv3 pass failed: {e}"
     fixed = args.config in ("fixed4k", "single")  # single: the same code on its 4 KiB chunks
     step_kernels = ("sorted_cost_kernel", "crc32c_sorted_kernel",  # the sorted path
-                    "plan_", "long_items", "crc32c_chunk_kernel", "crc32c_finalize", "long_finalize")
+                    "plan_", "long_items", "crc32c_chunk_kernel", "crc32c_finalize", "long_finalize",
+                    "crc32c_direct_kernel")
     vals = []
     for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
@@ -164,11 +176,44 @@ def pmc_traffic(args) -> tuple[float | None, str]:
     if fixed:
         return 2.0 * 1024.0 * float(np.median(vals)), \
             f"{len(vals)} dispatches, median, x2 gfx950 correction"
-    return 2.0 * 1024.0 * sum(vals) / PMC_CHILD_STEPS, \
-        f"sum over the step's dispatches / {PMC_CHILD_STEPS} steps, x2 gfx950 correction"
+    steps = PMC_CHILD_STEPS if args.config == "zipf" else 1
+    return 2.0 * 1024.0 * sum(vals) / steps, \
+        f"sum over the step's {len(vals) // steps} kernel dispatches ({steps} steps), x2 gfx950 " \
+        f"correction"
 
 
 PMC_CHILD_STEPS = 3
+
+
+def sub_args(args, config: str, **kw):
+    """A copy of the command's arguments for another workload (bench legs)."""
+    s = argparse.Namespace(**vars(args))
+    s.config = config
+    s.records_per_rank = 1 << 20
+    s.segments = None
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def usable_cpus() -> tuple[int, dict]:
+    cpus = host_cpus()
+    usable = cpus["affinity"]
+    if cpus["cgroup_quota_cpus"]:
+        usable = max(1, min(usable, int(cpus["cgroup_quota_cpus"])))
+    return usable, cpus
+
+
+def timed_rate(fn, nbytes: int, seconds: float) -> tuple[float, int]:
+    """GiB/s of fn() over nbytes, repeated for about `seconds` after one warm call."""
+    fn()
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return passes * nbytes / dt / 2**30, passes
 
 
 # ---- N > 1: the optional RCCL gather (SURVEY.md 8(e), BASELINE configs[3]) -----
@@ -371,6 +416,47 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
         g = gold.get("zipf_seed0x5eed_data0xda7a5eed_1048576", {})
         achieved = total / (ev * 1e-3) / 1e9
         on_sorted = E.stats().get("sorted_batches", 0) - sorted0 == args.steps
+        sustained = None
+        if args.leg_sustain_seconds > 0:
+            # back-to-back steps for a few seconds: a 20-step region is ~17 ms,
+            # so a clock transient moves it; this is the settled rate
+            E.sync()
+            E.timer_start()
+            n_s, t_s = 0, time.perf_counter()
+            while time.perf_counter() - t_s < args.leg_sustain_seconds:
+                for _ in range(50):
+                    E.device_batch(data, d_off, d_len, R, out, total_bytes=total, asynchronous=True)
+                n_s += 50
+                E.sync()
+            s_ms = E.timer_stop() / n_s
+            s_gbs = total / (s_ms * 1e-3) / 1e9
+            sustained = {"steps": n_s, "step_ms": round(s_ms, 4), "achieved_gb_s": round(s_gbs, 1),
+                         "frac": round(s_gbs / HBM_PEAK_GBS, 4),
+                         "digest_unchanged": E.crc32c_device(out, R * 4) == dig}
+        cpu = None
+        if not args.no_cpu:
+            # the reference over the first records of the same batch (<= 1 GiB,
+            # host DRAM), on every CPU this process may use
+            from oracle.oracle import Oracle, Reference, reference_available
+            if reference_available():
+                usable, cpus = usable_cpus()
+                k = int(np.searchsorted(np.cumsum(ln, dtype=np.uint64), np.uint64(1 << 30)))
+                nb = int(off[k - 1] + ln[k - 1])
+                hb = Oracle().fill(nb, W.DATA_SEED, 0)
+                ref = Reference()
+                want = ref.batch(hb, off[:k], ln[:k], threads=usable)
+                rate, passes = timed_rate(lambda: ref.batch(hb, off[:k], ln[:k], threads=usable),
+                                          nb, args.leg_cpu_seconds)
+                rate1, _ = timed_rate(lambda: ref.batch(hb, off[:k // 8], ln[:k // 8], threads=1),
+                                      int(off[k // 8]), args.leg_cpu_seconds / 2)
+                got = out.download(np.uint32, k)
+                cpu = {"value": round(rate, 2), "unit": "GiB/s", "cores": usable,
+                       "kind": "reference", "single_thread_value": round(rate1, 2),
+                       "sample": f"records 0..{k - 1} of the same batch ({nb / 2**30:.3f} GiB, host "
+                                 f"DRAM), consus::crc32c from common/crc32c.cc compiled unmodified, "
+                                 f"{passes} passes x {usable} std::threads; single thread over "
+                                 f"records 0..{k // 8 - 1}; cpu: {cpus['model']}",
+                       "matches_gpu": bool(np.array_equal(got, want))}
         res.update({
             "metric": "GiB/s CRC32C over device-resident mixed-length records (Zipf 64 B-64 KiB)",
             "value": round(total / (wall) / 2**30, 2), "unit": "GiB/s",
@@ -387,7 +473,7 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
                                     "sorted path)") if on_sorted else
                                    "plan + crc32c_chunk_kernel + finalize (whole step, piece path)"},
             "digest_verified": (dig == g.get("digest")) if g and R == 1 << 20 else None,
-            "digests": [f"{dig:#010x}"]})
+            "digests": [f"{dig:#010x}"], "sustained": sustained, "cpu_baseline": cpu})
         return res
     if args.config == "single":
         n = 1 << 32
@@ -460,6 +546,10 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
         ts = [pipe.submit(pb, fo, fl, o) for (pb, fo, fl), o in zip(segs, outs)]
         for t in ts:
             pipe.wait(t)
+    if args.child_pmc:
+        step()
+        pipe.close()
+        return {}
     for _ in range(args.warmup):
         step()
     t0 = time.perf_counter()
@@ -486,6 +576,38 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
         g = gold.get(f"fixed_4096_seed0xc0de_per_1048576", {})
         ok = (whole == g.get("block_digests", [None])[0]) if nseg * (W.SEGMENT_BYTES // RECORD) \
             == 1 << 20 else None
+    pipe.close()
+    cpu = None
+    if not args.no_cpu:
+        # the reference on the same host-resident segments (no link to cross):
+        # what txman's own cores would do with these buffers
+        from oracle.oracle import Reference, reference_available
+        if reference_available():
+            usable, cpus = usable_cpus()
+            ref = Reference()
+            if args.config == "stream":
+                frames = sum(int(fl.astype(np.uint64).sum()) for _, _, fl in segs)
+                run = lambda th: [ref.batch(pb.array, fo, fl, threads=th) for pb, fo, fl in segs]
+                ok_cpu = all(np.array_equal(ref.batch(pb.array, fo, fl, threads=usable), o)
+                             for (pb, fo, fl), o in zip(segs, outs))
+            else:
+                frames = total
+                per = W.SEGMENT_BYTES // RECORD
+                run = lambda th: [ref.fixed(pb.array, RECORD, RECORD, per, threads=th)
+                                  for pb, _, _ in segs]
+                ok_cpu = all(np.array_equal(ref.fixed(pb.array, RECORD, RECORD, per, threads=usable),
+                                            o) for (pb, _, _), o in zip(segs, outs))
+            rate, passes = timed_rate(lambda: run(usable), frames, args.leg_cpu_seconds)
+            t1 = time.perf_counter()
+            run(1)  # one single-thread pass
+            rate1 = frames / 2**30 / (time.perf_counter() - t1)
+            cpu = {"value": round(rate, 2), "unit": "GiB/s", "cores": usable, "kind": "reference",
+                   "single_thread_value": round(rate1, 2),
+                   "sample": f"the same {nseg} pinned host segments ({frames / 2**30:.3f} GiB of "
+                             f"checksummed bytes per pass), consus::crc32c from common/crc32c.cc "
+                             f"compiled unmodified, {passes} passes x {usable} std::threads, each "
+                             f"segment's records split by count; cpu: {cpus['model']}",
+                   "matches_gpu": ok_cpu}
     res.update({"metric": metric, "value": round(total / wall / 2**30, 2), "unit": "GiB/s",
                 "ms_per_step": round(wall * 1e3, 4),
                 "data": "synthetic (SURVEY.md 8(d)); segments pre-built in pinned host memory",
@@ -493,10 +615,13 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
                            "bytes_per_step": total},
                 "roofline": {"bound": "pcie", "achieved": round(total / wall / 1e9, 1),
                              "peak": 63.0, "unit": "GB/s",
-                             "frac": round(total / wall / 1e9 / 63.0, 4), "traffic": None,
-                             "note": "host link PCIe Gen5 x16, 63 GB/s spec"},
-                "digest_verified": ok})
-    pipe.close()
+                             "frac": round(total / wall / 1e9 / 63.0, 4),
+                             "traffic": None if traffic[0] is None else round(traffic[0]),
+                             "traffic_note": "HBM bytes read by the step's CRC kernels (PMC "
+                                             f"FETCH_SIZE): {traffic[1]}; the bound is the host "
+                                             "link, PCIe Gen5 x16, 63 GB/s spec",
+                             "link_bytes_per_step": total},
+                "digest_verified": ok, "cpu_baseline": cpu})
     return res
 
 
@@ -662,8 +787,16 @@ def main():
     # Traffic pass first, before this process touches the GPU.
     traffic, traffic_note = (None, "skipped")
     if rank == 0 and world == 1 and not args.child_pmc and not args.no_pmc and \
-            args.config in ("fixed4k", "zipf", "single"):
+            args.config in ("fixed4k", "zipf", "single", "stream", "pcie4k"):
         traffic, traffic_note = pmc_traffic(args)
+    # The other single-GPU BASELINE configs ride in the headline line (N = 1):
+    # configs[2], configs[4] and configs[1]'s bytes starting in host memory.
+    legs = []
+    if world == 1 and args.config == "fixed4k" and not args.child_pmc and not args.no_legs:
+        for key, cfg in (("config2_zipf", "zipf"), ("config4_stream", "stream"),
+                         ("config1_pcie_inclusive", "pcie4k")):
+            sub = sub_args(args, cfg)
+            legs.append((key, sub, pmc_traffic(sub) if not args.no_pmc else (None, "skipped")))
 
     if args.config == "dlog":  # a child process drives the engine; none here
         if rank == 0:
@@ -787,6 +920,20 @@ def main():
         if crcs_dev_digest != E.crc32c_device(out, R * 4):
             sustained["error"] = "CRC vector changed under sustained launches"
 
+    # the other single-GPU configs, while the clocks are warm (their CPU legs
+    # run after their own GPU timing)
+    leg_res = {}
+    for key, sub, tr in legs:
+        t_leg = time.perf_counter()
+        try:
+            r = run_secondary(sub, E, tr)
+            for k in ("n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
+                r.pop(k, None)
+        except Exception as e:  # noqa: BLE001 -- a leg must not lose the headline line
+            r = {"error": f"{type(e).__name__}: {e}"[:300]}
+        r["leg_wall_s"] = round(time.perf_counter() - t_leg, 2)
+        leg_res[key] = r
+
     total_bytes = world * R * L * args.steps
     value = total_bytes / wall / 2**30
     # per-GPU kernel rate; at N > 1 from the slowest rank's launches
@@ -830,6 +977,7 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(args)
     else:
         rec["cpu_baseline"] = None
+    rec.update(leg_res)
     if world > 1:
         rec["roofline"]["launch_ms_rank0"] = round(ev_ms / args.steps, 4)
         rec["gather"] = rccl_gather(E, dist, rank, world, out, R, digests, rec) \
