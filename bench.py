@@ -239,6 +239,9 @@ def rccl_gather(E, dist, rank: int, world: int, out, R: int, digests, rec) -> di
         uid = [E.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         E.comm_init(uid[0], world, rank)
+        info = E.comm_info()  # RCCL's own count of ranks and this rank's device
+        views = [None] * world
+        dist.all_gather_object(views, info)
         recv = E.DeviceBuffer(world * R * 4)
         E.comm_allgather_u32(out, R, recv)            # warm-up: connection setup
         times = []
@@ -251,11 +254,30 @@ def rccl_gather(E, dist, rank: int, world: int, out, R: int, digests, rec) -> di
                  for i in range(world)) if rank == 0 else None
         E.comm_destroy()
         res = {"collective": "rccl all-gather of u32 CRC vectors", "bytes_per_rank": R * 4,
-               "ms_median": round(1e3 * float(np.median(times)), 4), "verified": ok}
+               "ms_median": round(1e3 * float(np.median(times)), 4), "verified": ok,
+               "rccl_ranks": info["nranks"],
+               "rccl_devices": [v["device"] for v in views]}
+        if rank == 0 and (ok is not True or info["nranks"] != world):
+            res["error"] = f"gather check failed: verified={ok}, rccl_ranks={info['nranks']}"
     except Exception as e:  # noqa: BLE001 -- the gather is optional, the bench line is not
         res = {"collective": "rccl all-gather", "error": str(e)[:200]}
     done.set()
     return res
+
+
+def rank_identity(E, dist, rank: int, device: int, launch_ms: float) -> list | None:
+    """Every rank's (rank, HIP device, PCI bus id, per-launch ms), gathered on
+    the gloo control plane: the line shows which physical GPUs ran."""
+    try:
+        pci = E.device_pci_bus_id(device)
+    except Exception as e:  # noqa: BLE001
+        pci = f"unknown ({e})"[:60]
+    me = {"rank": rank, "device": device, "pci_bus_id": pci, "launch_ms": round(launch_ms, 4)}
+    if dist is None:
+        return [me]
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, me)
+    return allr
 
 
 # ---- CPU baseline: the reference itself ---------------------------------------
@@ -650,6 +672,8 @@ def run_single_split(args, E, dist, rank, world):
     t = torch.tensor([wall], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t[0])
+    ranks = rank_identity(E, dist, rank, 0 if args.share_device else
+                          int(os.environ.get("LOCAL_RANK", "0")), wall / args.steps * 1e3)
     t1 = time.perf_counter()
     whole = shard.gather_fold(crc, length)
     exch = time.perf_counter() - t1
@@ -676,6 +700,7 @@ def run_single_split(args, E, dist, rank, world):
                          "kernel": "per-rank slice: crc32c_span_chunk_kernel + single_tree + "
                                    "single_join (host sync included)"},
             "exchange_ms": round(exch * 1e3, 3),
+            "ranks": ranks, "distinct_gpus": len({r["pci_bus_id"] for r in ranks}),
             "digest_verified": (whole == want) if want is not None else None,
             "crc": f"{whole:#010x}", "cpu_baseline": None}), flush=True)
     dist.destroy_process_group()
@@ -736,6 +761,8 @@ def run_zipf_sharded(args, E, dist, rank, world):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, ev_max = float(t[0]), float(t[1])
     dig = E.crc32c_device(out, cnt * 4) if cnt else 0
+    ranks = rank_identity(E, dist, rank, 0 if args.share_device else
+                          int(os.environ.get("LOCAL_RANK", "0")), ev / args.steps)
     got = [None] * world
     dist.all_gather_object(got, (dig, cnt, local_total, ev, on_sorted))
     if rank == 0:
@@ -769,6 +796,7 @@ def run_zipf_sharded(args, E, dist, rank, world):
                                     else "plan + crc32c_chunk_kernel + finalize") +
                                    " (whole step; the slowest rank's bytes over its own step time)"},
             "digest_verified": ok, "digests": [f"{g[0]:#010x}" for g in got],
+            "ranks": ranks, "distinct_gpus": len({r["pci_bus_id"] for r in ranks}),
             "cpu_baseline": None}), flush=True)
     dist.destroy_process_group()
 
@@ -795,7 +823,9 @@ def main():
     if world == 1 and args.config == "fixed4k" and not args.child_pmc and not args.no_legs:
         for key, cfg in (("config2_zipf", "zipf"), ("config4_stream", "stream"),
                          ("config1_pcie_inclusive", "pcie4k")):
-            sub = sub_args(args, cfg)
+            # the zipf leg warms up for >= 100 steps (~80 ms): it starts after host-side
+            # preparation with the GPU idle, and 5 steps leave it in the clock ramp
+            sub = sub_args(args, cfg, **({"warmup": max(args.warmup, 100)} if cfg == "zipf" else {}))
             legs.append((key, sub, pmc_traffic(sub) if not args.no_pmc else (None, "skipped")))
 
     if args.config == "dlog":  # a child process drives the engine; none here
@@ -871,6 +901,7 @@ def main():
     else:
         ev_ms_max = ev_ms
 
+    ranks = rank_identity(E, dist, rank, 0 if args.share_device else local, ev_ms / args.steps)
     # Digest of this rank's CRC vector, computed on the GPU: crc32c(0, LE bytes).
     crcs_dev_digest = E.crc32c_device(out, R * 4)
     digests = [crcs_dev_digest]
@@ -881,9 +912,10 @@ def main():
 
     do_gather = dist is not None and not args.no_gather and not args.share_device
     if rank != 0:
-        if do_gather:
-            rccl_gather(E, dist, rank, world, out, R, digests, None)
+        g = rccl_gather(E, dist, rank, world, out, R, digests, None) if do_gather else None
         dist.destroy_process_group()
+        if g and g.get("error"):
+            sys.exit(4)
         return
 
     # golden digests of 1M-record blocks; a rank holding k whole blocks is
@@ -980,11 +1012,19 @@ def main():
     rec.update(leg_res)
     if world > 1:
         rec["roofline"]["launch_ms_rank0"] = round(ev_ms / args.steps, 4)
+        rec["ranks"] = ranks
+        rec["distinct_gpus"] = len({r["pci_bus_id"] for r in ranks})
         rec["gather"] = rccl_gather(E, dist, rank, world, out, R, digests, rec) \
             if do_gather else None
+        rec["rccl_ranks"] = rec["gather"].get("rccl_ranks") if rec["gather"] else None
     print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    # a failed or unverified RCCL gather, or ranks that did not land on distinct
+    # GPUs, must not pass silently: the line above says what, the exit code too
+    if world > 1 and ((rec["gather"] or {}).get("error") or
+                      (not args.share_device and rec["distinct_gpus"] != world)):
+        sys.exit(4)
 
 
 if __name__ == "__main__":

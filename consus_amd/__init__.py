@@ -36,7 +36,7 @@ FLAG_DEVICE = 0x1
 FLAG_ASYNC = 0x2
 FLAG_PLANNED = 0x4  # force plan -> chunks -> finalize (no one-launch direct kernel)
 FLAG_FALLBACK = 0x8  # host memory: complete on the engine's CPU path if the GPU fails (counted)
-FLAG_PACKED = 0x10  # device batches: records back to back in address order (stream path)
+MAX_DEVICES = 16
 ERANGE = -34
 MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D = 1, 2, 3
 
@@ -103,6 +103,10 @@ _SIGS = {
                                               C.c_int, C.c_uint64]),
     "mi_crc32c_balanced_ranges": (None, [C.c_void_p, C.c_size_t, C.c_int, C.c_uint64,
                                          C.c_void_p]),
+    "mi_crc32c_set_gpu_min": (C.c_uint64, [C.c_uint64]),
+    "mi_crc32c_gpu_min": (C.c_uint64, []),
+    "mi_crc32c_device_pci_bus_id": (C.c_int, [C.c_int, C.c_char_p, C.c_int]),
+    "mi_comm_info": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
 }
 
 
@@ -110,10 +114,12 @@ class Stats(C.Structure):
     """mi_crc32c_stats_t (include/consus_crc32c.h)."""
     _fields_ = [("gpu_calls", C.c_uint64), ("fallback_calls", C.c_uint64),
                 ("fallback_bytes", C.c_uint64), ("sharded_calls", C.c_uint64),
-                ("stream_batches", C.c_uint64),
+                ("host_routed_calls", C.c_uint64),
                 ("last_fallback_status", C.c_int32),
-                ("reserved", C.c_int32),
-                ("sorted_batches", C.c_uint64)]
+                ("last_multi_ranges", C.c_int32),
+                ("sorted_batches", C.c_uint64),
+                ("host_routed_bytes", C.c_uint64),
+                ("last_multi_devices", C.c_int32 * MAX_DEVICES)]
 
 _lib = None
 
@@ -191,7 +197,7 @@ def crc32c_dropin(init_crc: int, data) -> int:
 
 
 def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False,
-                 fallback: bool = False, packed: bool = False) -> np.ndarray:
+                 fallback: bool = False) -> np.ndarray:
     """Per-record CRCs of host records [buf + off, +len)."""
     a = _as_u8(buf)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -205,8 +211,7 @@ def crc32c_batch(buf, offsets, lengths, inits=None, planned: bool = False,
     _check(lib().mi_crc32c_batch(C.c_void_p(a.ctypes.data), _np_ptr(off), _np_ptr(ln),
                                  _np_ptr(ini), off.size, int(ln.sum(dtype=np.uint64)),
                                  _np_ptr(out), (FLAG_PLANNED if planned else 0) |
-                                 (FLAG_FALLBACK if fallback else 0) |
-                                 (FLAG_PACKED if packed else 0)), "mi_crc32c_batch")
+                                 (FLAG_FALLBACK if fallback else 0)), "mi_crc32c_batch")
     return out
 
 
@@ -224,10 +229,29 @@ def crc32c_fixed(buf, stride: int, length: int, count: int, inits=None,
 
 
 def stats() -> dict:
-    """Process-wide counters: GPU-completed calls and CPU-path fallbacks."""
+    """Process-wide counters: GPU-completed calls, CPU-path fallbacks, size-routed
+    host calls, and the device ordinals of the last multi-device call."""
     s = Stats()
     lib().mi_crc32c_stats(C.byref(s))
-    return {f: int(getattr(s, f)) for f, _ in Stats._fields_ if f != "reserved"}
+    d = {f: int(getattr(s, f)) for f, _ in Stats._fields_ if f != "last_multi_devices"}
+    d["last_multi_devices"] = [int(x) for x in s.last_multi_devices[:max(s.last_multi_ranges, 0)]]
+    return d
+
+
+def set_gpu_min(nbytes: int) -> int:
+    """Single host calls below nbytes run on the CPU path (size routing); 0 =
+    every call on the GPU.  Returns the previous threshold."""
+    return int(lib().mi_crc32c_set_gpu_min(int(nbytes)))
+
+
+def gpu_min() -> int:
+    return int(lib().mi_crc32c_gpu_min())
+
+
+def device_pci_bus_id(device: int) -> str:
+    buf = C.create_string_buffer(64)
+    _check(lib().mi_crc32c_device_pci_bus_id(device, buf, 64), "mi_crc32c_device_pci_bus_id")
+    return buf.value.decode()
 
 
 def stats_reset() -> None:
@@ -353,8 +377,8 @@ def device_batch_fixed(data: DeviceBuffer, stride: int, length: int, count: int,
 
 def device_batch(data: DeviceBuffer, offsets: DeviceBuffer, lengths: DeviceBuffer, count: int,
                  out: DeviceBuffer, inits: DeviceBuffer | None = None, total_bytes: int = 0,
-                 asynchronous: bool = False, packed: bool = False) -> None:
-    flags = FLAG_DEVICE | (FLAG_ASYNC if asynchronous else 0) | (FLAG_PACKED if packed else 0)
+                 asynchronous: bool = False) -> None:
+    flags = FLAG_DEVICE | (FLAG_ASYNC if asynchronous else 0)
     _check(lib().mi_crc32c_batch(C.c_void_p(data.ptr), C.c_void_p(offsets.ptr),
                                  C.c_void_p(lengths.ptr),
                                  None if inits is None else C.c_void_p(inits.ptr), count,
@@ -478,6 +502,14 @@ def comm_allgather_u32(send: DeviceBuffer, count: int, recv: DeviceBuffer) -> No
         raise ValueError("send buffer too small")
     _check(lib().mi_comm_allgather_u32(C.c_void_p(send.ptr), count, C.c_void_p(recv.ptr)),
            "mi_comm_allgather_u32")
+
+
+def comm_info() -> dict:
+    """RCCL's own view of the communicator: ranks (ncclCommCount), this rank,
+    and the HIP device it drives."""
+    n, r, d = C.c_int(0), C.c_int(0), C.c_int(0)
+    _check(lib().mi_comm_info(C.byref(n), C.byref(r), C.byref(d)), "mi_comm_info")
+    return {"nranks": int(n.value), "rank": int(r.value), "device": int(d.value)}
 
 
 def comm_destroy() -> None:

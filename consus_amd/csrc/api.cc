@@ -2,6 +2,9 @@
 // (include/consus_crc32c.h) above the HIP engine (engine.hip):
 //
 //   * argument checks and the per-thread error message;
+//   * size routing: single host calls below the GPU threshold
+//     (mi_crc32c_set_gpu_min) are answered by the CPU path without a GPU
+//     round trip, counted as host_routed_calls;
 //   * totality: the drop-in mi_crc32c / consus::crc32c never fails, as the
 //     reference cannot (common/crc32c.cc:122-126).  When the engine reports a
 //     failure (no usable device, a HIP error, an input beyond its limits) the
@@ -23,6 +26,8 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -66,6 +71,23 @@ uint64_t shard_min(uint64_t arg)
     return env ? env : kShardMinDefault;
 }
 
+// Single host calls below this many bytes are answered on the CPU (size
+// routing).  Measured on MI355X + EPYC 9575F (tools/route_probe.cc,
+// profiles/r03_route_probe.txt): a GPU round trip of
+// one host call costs 17 us at 16 B, 21 us at 4 KiB, 117 us at 1 MiB and
+// 154 us at 4 MiB (pageable staging); the CPU path runs at ~13 GiB/s (0.03 us
+// at 16 B, 78 us at 1 MiB, 313 us at 4 MiB).  They cross near 1.7 MiB.
+constexpr uint64_t kGpuMinDefault = uint64_t(3) << 19;  // 1.5 MiB
+
+std::atomic<uint64_t>& gpu_min_word()
+{
+    static std::atomic<uint64_t> w{[] {
+        const char* e = std::getenv("MI_CRC32C_GPU_MIN");
+        return e ? uint64_t(std::strtoull(e, nullptr, 0)) : kGpuMinDefault;
+    }()};
+    return w;
+}
+
 // A failure the CPU path can stand in for: anything but a bad argument.
 bool engine_failure(int st) { return st != MI_CRC32C_OK && st != MI_CRC32C_EINVAL; }
 
@@ -84,14 +106,25 @@ uint64_t sum_lengths(const uint32_t* lengths, size_t count)
 class Workers
 {
   public:
-    // Runs jobs[0] on the calling thread and jobs[1..] on workers; waits for all.
+    // Runs jobs[0] on the calling thread and jobs[1..] on workers; waits for
+    // all of them before returning, even if jobs[0] throws (the workers hold
+    // pointers into `jobs`).  Jobs catch their own exceptions (guarded()).
     void run(std::vector<std::function<void()>>& jobs)
     {
         std::lock_guard<std::mutex> call(m_call);
         while (m_ws.size() + 1 < jobs.size()) m_ws.emplace_back(new Worker);
-        for (size_t j = 1; j < jobs.size(); ++j) m_ws[j - 1]->post(&jobs[j]);
+        size_t posted = 0;
+        struct JoinAll
+        {
+            Workers* w;
+            const size_t* n;
+            ~JoinAll()
+            {
+                for (size_t j = 0; j < *n; ++j) w->m_ws[j]->join();
+            }
+        } join_all{this, &posted};
+        for (size_t j = 1; j < jobs.size(); ++j, ++posted) m_ws[j - 1]->post(&jobs[j]);
         jobs[0]();
-        for (size_t j = 1; j < jobs.size(); ++j) m_ws[j - 1]->join();
     }
 
   private:
@@ -141,6 +174,33 @@ Workers& workers()
 {
     static Workers* w = new Workers;  // leaked on purpose (see Workers)
     return *w;
+}
+
+// A job body that never lets an exception escape (it would cross the C ABI,
+// or kill a worker thread): std::bad_alloc maps to ENOMEM, anything else to
+// EHIP, recorded in the job's status slot.
+template <typename F>
+void guarded(int& status, std::string& msg, F&& body)
+{
+    try
+    {
+        body();
+    }
+    catch (const std::bad_alloc&)
+    {
+        status = MI_CRC32C_ENOMEM;
+        msg = "out of host memory";
+    }
+    catch (const std::exception& e)
+    {
+        status = MI_CRC32C_EHIP;
+        msg = e.what();
+    }
+    catch (...)
+    {
+        status = MI_CRC32C_EHIP;
+        msg = "unknown exception";
+    }
 }
 
 // MI_CRC32C_DEVICES="0,1,2,3": the device list multi-device calls use when
@@ -224,8 +284,19 @@ int mi_crc32c_device_count(void)
     return mi_eng::usable_devices(ords, mi_eng::kMaxDevices);
 }
 
+uint64_t mi_crc32c_set_gpu_min(uint64_t gpu_min) { return gpu_min_word().exchange(gpu_min); }
+
+uint64_t mi_crc32c_gpu_min(void) { return gpu_min_word().load(std::memory_order_relaxed); }
+
 int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, unsigned flags)
 {
+    if (!(flags & MI_CRC32C_DEVICE) && n && n < gpu_min_word().load(std::memory_order_relaxed))
+    {
+        if (!out || !data) return fail(MI_CRC32C_EINVAL, "null pointer");
+        *out = mi_host::crc32c(init, data, n);
+        mi_host::note_host_routed(n);
+        return MI_CRC32C_OK;
+    }
     const int st = mi_eng::buffer(-1, init, data, n, out, flags);
     if (st == MI_CRC32C_OK)
     {
@@ -242,6 +313,12 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
 uint32_t mi_crc32c(uint32_t init, const void* data, size_t n)
 {
     if (n == 0) return init;
+    // too small to pay a GPU round trip: the CPU path, by design (counted)
+    if (n < gpu_min_word().load(std::memory_order_relaxed))
+    {
+        mi_host::note_host_routed(n);
+        return mi_host::crc32c(init, data, n);
+    }
     uint32_t out = 0;
     const int st = mi_eng::buffer(-1, init, data, n, &out, 0);
     if (st == MI_CRC32C_OK)
@@ -319,7 +396,7 @@ int mi_crc32c_batch_multi(const void* base, const uint64_t* offsets, const uint3
     std::vector<std::string> msgs(static_cast<size_t>(k));
     std::vector<std::function<void()>> jobs;
     for (int j = 0; j < k; ++j)
-        jobs.emplace_back([&, j] {
+        jobs.emplace_back([&, j] { guarded(status[size_t(j)], msgs[size_t(j)], [&] {
             const size_t lo = bounds[size_t(j)], n = bounds[size_t(j) + 1] - lo;
             if (n == 0) return;
             const uint64_t bytes = sum_lengths(lengths + lo, n);
@@ -337,7 +414,8 @@ int mi_crc32c_batch_multi(const void* base, const uint64_t* offsets, const uint3
                 mi_host::note_gpu_call();
             status[size_t(j)] = st;
             if (st != MI_CRC32C_OK) msgs[size_t(j)] = mi_eng::t_err;
-        });
+        }); });
+    mi_host::note_multi(k, devs);
     if (k == 1)
         jobs[0]();
     else
@@ -380,7 +458,7 @@ int mi_crc32c_batch_fixed_multi(const void* base, uint64_t stride, uint64_t leng
     std::vector<std::function<void()>> jobs;
     const uint8_t* b = static_cast<const uint8_t*>(base);
     for (int j = 0; j < k; ++j)
-        jobs.emplace_back([&, j] {
+        jobs.emplace_back([&, j] { guarded(status[size_t(j)], msgs[size_t(j)], [&] {
             const size_t lo = count * size_t(j) / size_t(k), hi = count * size_t(j + 1) / size_t(k);
             if (hi == lo) return;
             int st = mi_eng::batch_fixed(devs[j], b + lo * stride, stride, length,
@@ -397,7 +475,8 @@ int mi_crc32c_batch_fixed_multi(const void* base, uint64_t stride, uint64_t leng
                 mi_host::note_gpu_call();
             status[size_t(j)] = st;
             if (st != MI_CRC32C_OK) msgs[size_t(j)] = mi_eng::t_err;
-        });
+        }); });
+    mi_host::note_multi(k, devs);
     if (k == 1)
         jobs[0]();
     else

@@ -126,24 +126,6 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
                          uint32_t* out, const uint32_t* tables, const uint32_t* pow2, int grid,
                          hipStream_t stream);
 
-// Batches of records in address order hashed as one stream of aligned 4 KiB
-// chunks over [base + offsets[0], + span) (launch_stream).
-constexpr uint32_t kStreamCtrlWords = 16;
-struct StreamWorkspace
-{
-    uint32_t* ctrl;   // kStreamCtrlWords, immediately followed by the row masks (one memset)
-    uint32_t* masks;  // stream_max_chunks(span)
-    uint32_t* R;      // stream_max_chunks(span): raw register of each chunk
-    uint4* snaps;     // stream_max_chunks(span) * 32 rows * 8 lanes: chain snapshots (sparse)
-    uint32_t* pval;   // 2 * count: prefix registers at record starts and ends
-    uint32_t* longs;  // count
-};
-uint64_t stream_max_chunks(uint64_t span);
-hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32_t* lengths,
-                         const uint32_t* inits, uint64_t count, uint64_t span,
-                         const StreamWorkspace& ws, uint32_t* out, const uint32_t* tables,
-                         const uint32_t* pow2, int cus, hipStream_t stream);
-
 hipError_t launch_chain(const uint32_t* crcs, const uint64_t* after, uint32_t np, uint32_t* out,
                         const uint32_t* pow2_tables, hipStream_t stream);
 hipError_t launch_combine(const uint32_t* crc_a, const uint32_t* crc_b, const uint64_t* len_b,

@@ -24,17 +24,6 @@
 
 #include "crc32c_kernels.h"
 
-// Ablation modes for tools/ablate.py (the product build is mode 0):
-//   1 = skip the LDS table staging, 2 = no global loads (synthetic data),
-//   4 = no table lookups (data XORed straight into the chains),
-//   8 = address builds kept, each lookup replaced by one VALU op,
-//   16 = team fold replaced by an XOR of the chains.
-// Results are wrong in any mode != 0; only the timing is meaningful.
-#ifndef MI_CRC_ABLATE
-#define MI_CRC_ABLATE 0
-#endif
-
-
 namespace mi_crc {
 
 extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -62,7 +51,6 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 //   (t >> 1) * 65536 + b * 256 + (t & 1) * 128 + c * 4   ->  bank == c.
 __device__ __forceinline__ void stage_tables(const uint32_t* __restrict__ g)
 {
-    if (MI_CRC_ABLATE & 1) return;
     // Every record kernel runs kBlock threads: all loads are issued first,
     // then all stores (one L2 round trip per thread, not one per iteration).
     constexpr uint32_t NM = 1024u * 8u / kBlock;          // G^{128} entries x 8 quads
@@ -136,14 +124,6 @@ __device__ __forceinline__ uint32_t zG(uint32_t base, uint32_t v)
 // conflict-free ds_read_b32 in flight per row.
 __device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint32_t li)
 {
-    if (MI_CRC_ABLATE & 4)
-    {
-        V[0] = (V[0] >> 1) ^ d.x;
-        V[1] = (V[1] >> 1) ^ d.y;
-        V[2] = (V[2] >> 1) ^ d.z;
-        V[3] = (V[3] >> 1) ^ d.w;
-        return;
-    }
     uint32_t a[16], r[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -155,7 +135,7 @@ __device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-        r[i] = (MI_CRC_ABLATE & 8) ? (a[i] ^ (a[i] >> 3)) : lds32(kLdsMain + a[i]);
+        r[i] = lds32(kLdsMain + a[i]);
     V[0] = xor3(xor3(r[0], r[1], r[2]), r[3], d.x);
     V[1] = xor3(xor3(r[4], r[5], r[6]), r[7], d.y);
     V[2] = xor3(xor3(r[8], r[9], r[10]), r[11], d.z);
@@ -165,9 +145,6 @@ __device__ __forceinline__ void row_update(uint32_t (&V)[4], const uint4 d, uint
 // The first row of a record meets all-zero chains, whose lookups are all
 // G[0] = 0: the update is the row itself (saves the row's 16 lookups, 16
 // address builds and 8 XORs: one row in 32 of a 4 KiB record).
-#ifndef MI_FIRST_ROW_COPY
-#define MI_FIRST_ROW_COPY 1
-#endif
 __device__ __forceinline__ void row_first(uint32_t (&V)[4], const uint4 d)
 {
     V[0] = d.x;
@@ -190,41 +167,21 @@ __device__ __forceinline__ uint32_t from_lane_up(uint32_t v)
     return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x100 + N, 0xF, 0xF, true));
 }
 
-#ifndef MI_FOLD_MASK
-#define MI_FOLD_MASK 0
-#endif
 __device__ __forceinline__ uint32_t team_fold(const uint32_t (&V)[4])
 {
-    if (MI_CRC_ABLATE & 16) return V[0] ^ V[1] ^ V[2] ^ V[3];
     const uint32_t x = zT<4>(V[0]) ^ zT<3>(V[1]) ^ zT<2>(V[2]) ^ zT<1>(V[3]);
-#if MI_FOLD_MASK
-    // the tree's lookups only in the lanes whose result is used (fewer lanes
-    // per ds_read_b32, fewer bank conflicts); the DPP reads stay unmasked
-    const uint32_t u1 = from_lane_up<1>(x);
-    uint32_t y = 0, w = 0, r = 0;
-    if (!(threadIdx.x & 1u)) y = zT<4>(x) ^ u1;
-    const uint32_t u2 = from_lane_up<2>(y);
-    if (!(threadIdx.x & 3u)) w = zG(kLdsZ32, y) ^ u2;
-    const uint32_t u4 = from_lane_up<4>(w);
-    if (!(threadIdx.x & 7u)) r = zG(kLdsZ64, w) ^ u4;
-    return r;
-#else
     const uint32_t y = zT<4>(x) ^ from_lane_up<1>(x);
     const uint32_t w = zG(kLdsZ32, y) ^ from_lane_up<2>(y);
     return zG(kLdsZ64, w) ^ from_lane_up<4>(w);
-#endif
 }
 
-// The same fold without LDS tables (MI_FOLD_LANE): every Z_n of the fold is
+// The same fold without LDS tables (the headline kernel's): every Z_n of the fold is
 // six 64-entry tables of 6-bit slices (kTabLane), each held one entry per lane
 // in a VGPR and read with ds_bpermute, a crossbar permute that touches no LDS
 // bank.  The shared slice-by-16 tables cannot be made bank-private (24 KiB of
 // them beside the 128 KiB G^{128} image), so their random lookups conflict
 // 3.5-way on average; these cannot conflict.  The permute uses address bits
 // 7:2 only, so each slice's address is one shift.  Costs 36 VGPRs.
-#ifndef MI_FOLD_LANE
-#define MI_FOLD_LANE 1
-#endif
 struct LaneTabs
 {
     uint32_t t[36];
@@ -250,7 +207,6 @@ __device__ __forceinline__ uint32_t zL(const LaneTabs& L, uint32_t v)
 // Every lane of the wave must be active (ds_bpermute reads inactive lanes as 0).
 __device__ __forceinline__ uint32_t team_fold_lane(const uint32_t (&V)[4], const LaneTabs& L)
 {
-    if (MI_CRC_ABLATE & 16) return V[0] ^ V[1] ^ V[2] ^ V[3];
     const uint32_t x = zL<0>(L, V[0]) ^ zL<1>(L, V[1]) ^ zL<2>(L, V[2]) ^ zL<3>(L, V[3]);
     const uint32_t y = zL<0>(L, x) ^ from_lane_up<1>(x);
     const uint32_t w = zL<4>(L, y) ^ from_lane_up<2>(y);
@@ -271,11 +227,6 @@ __device__ __forceinline__ u32x4_t make_u32x4(const uint4& v)
 
 __device__ __forceinline__ uint4 load16(const uint8_t* p)
 {
-    if (MI_CRC_ABLATE & 2)
-    {
-        const uint32_t a = uint32_t(uintptr_t(p));
-        return make_uint4(a, a * 3u, a ^ 0x55u, a + 7u);
-    }
     // explicitly global: a pointer rebuilt from an integer (Item::bits) would
     // otherwise be FLAT, and FLAT loads also count in lgkmcnt, so every wait
     // for an LDS lookup would drain the prefetched rows too
@@ -394,15 +345,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_fixed_kernel(
 // 0.652-0.669.  Issuing one row ahead of each row's folding spreads the loads
 // evenly through the lookups; the depth beyond 3 rows changes nothing.
 // Dropping the sched_barrier costs 1 % (Q = 1, NB = 4: 0.649-0.655).
-#ifndef MI_PIPE_ROWS
-#define MI_PIPE_ROWS 1
-#endif
-#ifndef MI_PIPE_BUFS
-#define MI_PIPE_BUFS 4
-#endif
-#ifndef MI_PIPE_EARLY
-#define MI_PIPE_EARLY 0
-#endif
+// Issuing the first record's rows before the table staging was neutral
+// (0.636-0.658 vs 0.634-0.658 ms, 6 interleaved rounds).
+constexpr int kPipeRows = 1, kPipeBufs = 4;
 template <int G, bool INITS>
 __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uint64_t stride,
                                            const uint32_t* __restrict__ inits,
@@ -410,7 +355,7 @@ __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uin
                                            uint32_t* __restrict__ out,
                                            const uint32_t* __restrict__ tables)
 {
-    constexpr int Q = MI_PIPE_ROWS, NB = MI_PIPE_BUFS;
+    constexpr int Q = kPipeRows, NB = kPipeBufs;
     constexpr int SG = G * kGroupRows / Q;  // sub-groups per record
     static_assert(G * kGroupRows % Q == 0 && SG % NB == 0 && NB >= 2, "pipeline shape");
     const uint32_t tl = threadIdx.x & (kTeam - 1);
@@ -430,30 +375,16 @@ __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uin
         for (int r = 0; r < Q; ++r) buf[r] = load16(p + r * kRowBytes);
     };
 
-    // MI_PIPE_EARLY=1 issues the first record's rows before the table
-    // staging (its barrier waits for LDS only, so HBM would stream while the
-    // tables are copied in): bit-exact, 92 VGPRs, measured neutral (6
-    // interleaved rounds, 0.636-0.658 vs 0.634-0.658 ms min), so off.
     uint4 bufs[NB][Q];
     uint64_t rec = iters ? rec_of(0) : 0;
     uint32_t init_word = 0;
-    if (MI_PIPE_EARLY && iters)
-    {
-#pragma unroll
-        for (int q = 0; q < NB - 1; ++q) load_sub(bufs[q], rec, q);
-    }
     stage_tables(tables);  // every thread reaches the barrier
-#if MI_FOLD_LANE
     LaneTabs lt;
     load_lane_tabs(lt, tables);
-#endif
     if (iters == 0) return;
     if (INITS) init_word = inits[rec * init_stride];
-    if (!MI_PIPE_EARLY)
-    {
 #pragma unroll
-        for (int q = 0; q < NB - 1; ++q) load_sub(bufs[q], rec, q);
-    }
+    for (int q = 0; q < NB - 1; ++q) load_sub(bufs[q], rec, q);
     for (uint64_t it = 0; it < iters; ++it)
     {
         const uint64_t next = rec_of(it + 1);
@@ -472,25 +403,19 @@ __device__ __forceinline__ void fixed_pipe(const uint8_t* __restrict__ base, uin
             }
             // Keep the loads ahead of this sub-group's folding (the scheduler
             // would otherwise sink them into it to save registers).
-#ifndef MI_PIPE_NOSB
             __builtin_amdgcn_sched_barrier(0);
-#endif
             uint4(&cur)[Q] = bufs[q % NB];
             if (q == 0) cur[0].x ^= tl == 0 ? ~init_word : 0u;
 #pragma unroll
             for (int r = 0; r < Q; ++r)
             {
-                if (MI_FIRST_ROW_COPY && q == 0 && r == 0)
+                if (q == 0 && r == 0)
                     row_first(V, cur[0]);
                 else
                     row_update(V, cur[r], li);
             }
         }
-#if MI_FOLD_LANE
         const uint32_t raw = team_fold_lane(V, lt);
-#else
-        const uint32_t raw = team_fold(V);
-#endif
         if (tl == 0 && team + it * nteams < count) out[rec] = ~raw;
         rec = next;
         if (INITS) init_word = next_init;
@@ -579,10 +504,7 @@ hipError_t launch_fixed(const void* base, uint64_t stride, uint32_t len, const u
 // counts live in blk[bin * nblocks + block]; the plan header follows them
 // (plan_hdr): bin starts [0, kBins), total items, long-record count.
 constexpr uint32_t kPlanThreads = 1024;
-#ifndef MI_PLAN_PER
-#define MI_PLAN_PER 4
-#endif
-constexpr uint32_t kPlanPer = MI_PLAN_PER;
+constexpr uint32_t kPlanPer = 4;
 constexpr uint32_t kPlanRecs = kPlanThreads * kPlanPer;
 constexpr uint32_t kHdrTotal = kPlanHdrTotal;
 constexpr uint32_t kHdrLongs = kBins + 1;
@@ -1131,7 +1053,7 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
                     if (g == G - 1 && r == kGroupRows - 1) d = mask_below(d, cur.ce);
                     // the window's first row, or (one-group pieces) the first
                     // row some team of the wave needs: the chains are still zero
-                    if (MI_FIRST_ROW_COPY && g == 0 && (r == 0 || (G == 1 && fresh)))
+                    if (g == 0 && (r == 0 || (G == 1 && fresh)))
                         row_first(V, d);
                     else
                         row_update(V, d, li);
@@ -1145,87 +1067,6 @@ __device__ __forceinline__ void chunk_bin(const Item* __restrict__ items, uint32
             nit = nnit;
         }
     }
-}
-
-#ifndef MI_CHUNK_RING
-#define MI_CHUNK_RING 0  // bit G-1: the bins of G groups that take the row ring (measured: none)
-#endif
-// The same work with the fixed kernel's row pipeline (fixed_pipe, Q = 1,
-// NB = 4): each row is issued three rows ahead of its folding, across item
-// boundaries (the next item's first rows are issued during this item's last
-// rows), descriptors two items ahead.  Every item has 8 G rows, a multiple of
-// the ring, so every buffer's role is the same in every item and vmcnt stays
-// exact.
-#ifndef MI_CHUNK_RING_NB4
-#define MI_CHUNK_RING_NB4 8  // ring depth of the 4-group bin (its 4 lead waves per CU need depth)
-#endif
-template <int G>
-__device__ __forceinline__ void chunk_bin_ring(const Item* __restrict__ items, uint32_t lo,
-                                               uint32_t hi, uint32_t* __restrict__ partial,
-                                               uint32_t team, uint32_t team0, uint32_t nteams,
-                                               uint32_t tl, uint32_t li, const uint8_t* zero16)
-{
-    if (hi <= lo || lo + team0 >= hi) return;
-    constexpr int RR = G * kGroupRows, NB = G == 4 ? MI_CHUNK_RING_NB4 : 4, AHEAD = NB - 1;
-    static_assert(RR % NB == 0, "ring roles per item");
-    const uint32_t iters = (hi - lo - team0 + nteams - 1) / nteams;
-    auto idx_of = [&](uint32_t k) {
-        const uint32_t i = lo + team + k * nteams;
-        return i < hi ? i : hi - 1;
-    };
-    // group-0 blocks wholly before the piece read a zero block
-    auto row_ptr = [&](const ChunkView& v, int r) {
-        const int32_t o = r * int32_t(kRowBytes);
-        return (r < kGroupRows && v.x + o <= -16) ? zero16 : v.p0 + o;
-    };
-    uint4 buf[NB];
-    ChunkView cur = view_of<G>(items[idx_of(0)], tl);
-    Item nit = items[idx_of(1)];
-#pragma unroll
-    for (int r = 0; r < AHEAD; ++r) buf[r] = load16(row_ptr(cur, r));
-    for (uint32_t k = 0; k < iters; ++k)
-    {
-        const Item nnit = items[idx_of(k + 2)];
-        const ChunkView nxt = view_of<G>(nit, tl);
-        uint32_t V[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int r = 0; r < RR; ++r)
-        {
-            const int ra = r + AHEAD;
-            buf[ra % NB] = load16(ra < RR ? row_ptr(cur, ra) : row_ptr(nxt, ra - RR));
-            __builtin_amdgcn_sched_barrier(0);
-            uint4 d = buf[r % NB];
-            if (r < kGroupRows)
-            {
-                // rows before every team's piece leave V = 0: skip them
-                // (one-group pieces are sorted by row count, so this is common)
-                if (G == 1 && !__builtin_amdgcn_ballot_w64(cur.x + r * int32_t(kRowBytes) > -16))
-                    continue;
-                const bool start_here = (cur.rsb >> 4) == r;
-                if (__builtin_amdgcn_ballot_w64(start_here))
-                    d = mask_from(d, start_here ? (cur.rsb & 15) : 0);
-            }
-            if (r == RR - 1) d = mask_below(d, cur.ce);
-            row_update(V, d, li);
-        }
-        const uint32_t raw = team_fold(V);
-        const uint32_t i = lo + team + k * nteams;
-        if (tl == 0 && i < hi) partial[i] = raw;
-        cur = nxt;
-        nit = nnit;
-    }
-}
-
-template <int G>
-__device__ __forceinline__ void chunk_bin_any(const Item* __restrict__ items, uint32_t lo,
-                                              uint32_t hi, uint32_t* __restrict__ partial,
-                                              uint32_t team, uint32_t team0, uint32_t nteams,
-                                              uint32_t tl, uint32_t li, const uint8_t* zero16)
-{
-    if (MI_CHUNK_RING & (1 << (G - 1)))
-        chunk_bin_ring<G>(items, lo, hi, partial, team, team0, nteams, tl, li, zero16);
-    else
-        chunk_bin<G>(items, lo, hi, partial, team, team0, nteams, tl, li, zero16);
 }
 
 // All bins in one launch with wave roles.  Measured on config 3 (MI355X):
@@ -1278,16 +1119,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
     {
         const uint32_t team = (blockIdx.x * lead + wave) * kTeam + tw;
         const uint32_t nteams = gridDim.x * lead * kTeam;
-        chunk_bin_any<4>(items, b0, split, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin<4>(items, b0, split, partial, team, team & ~7u, nteams, tl, li, zero16);
     }
     else
     {
         const uint32_t rest = 16u - lead;
         const uint32_t team = (blockIdx.x * rest + (wave - lead)) * kTeam + tw;
         const uint32_t nteams = gridDim.x * rest * kTeam;
-        chunk_bin_any<3>(items, b1, b2, partial, team, team & ~7u, nteams, tl, li, zero16);
-        chunk_bin_any<2>(items, b2, b3, partial, team, team & ~7u, nteams, tl, li, zero16);
-        chunk_bin_any<1>(items, b3, n_items, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin<3>(items, b1, b2, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin<2>(items, b2, b3, partial, team, team & ~7u, nteams, tl, li, zero16);
+        chunk_bin<1>(items, b3, n_items, partial, team, team & ~7u, nteams, tl, li, zero16);
     }
     // one relaxed atomic per wave grab; every wave leaves once the pool is empty
     while (split < b1)
@@ -1298,7 +1139,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_chunk_kernel(
                                          __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t lo = split + __builtin_amdgcn_readfirstlane(got);
         if (lo >= b1) break;
-        chunk_bin_any<4>(items, lo, min(lo + kGrab, b1), partial, tw, 0u, 64u / kTeam, tl, li, zero16);
+        chunk_bin<4>(items, lo, min(lo + kGrab, b1), partial, tw, 0u, 64u / kTeam, tl, li, zero16);
     }
 }
 
@@ -1553,7 +1394,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
                 uint4 d = buf[k];
                 if (row == 0) d = mask_from(d, f0);
                 if (row + 1 == rows) d = mask_below(d, bl);
-                if (MI_FIRST_ROW_COPY && row == 0)
+                if (row == 0)
                     row_first(V, d);
                 else
                     row_update(V, d, li);
@@ -1877,407 +1718,6 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
 }
 
 // ---------------------------------------------------------------------------
-// Sorted batches as one stream.  When the records
-// are in address order and do not overlap -- offsets[i + 1] >= offsets[i] +
-// lengths[i]: a durable-log segment (frames with their 4-byte CRC slots
-// between them), BASELINE configs[2] -- the batch lies in the byte range
-// [lo, lo + span) with lo = base + offsets[0], and is hashed as the aligned
-// 4 KiB chunks that cover it, exactly as the headline kernel hashes 4 KiB
-// records: no pieces, no masks, every byte read once.  A record boundary x
-// inside chunk k needs the prefix register P_k(x) = raw(chunk[0, x)): the
-// chunk pass stores its team's 32 chain registers (128 B) before every row
-// that holds a boundary (row masks from stream_mark_kernel),
-// stream_points_kernel folds that snapshot with the boundary's row masked
-// to the bytes before x, and stream_finalize_kernel chains chunk registers
-// and prefixes per record [a, E):
-//   s = ~init ^ P(a);  one chunk: s = Z_{E-a}(s) ^ P(E)
-//   else s = Z_{4096-xa}(s) ^ R[k0];  s = Z_4096(s) ^ R[k]  (interior);
-//        s = Z_{xe}(s) ^ P(E);  crc = ~s
-// Bytes of the first and last chunk outside the records (and in the gaps
-// between them) cancel out of every record's value; the whole 4 KiB page of
-// a valid byte is readable.  Boundary points: 2i = start of record i, 2i + 1
-// = its end; an end equal to the next record's start is not computed twice
-// (the finalize reads the start).  Control words (zeroed with the masks by
-// one memset): kStrErr = order violated (every record is then hashed
-// byte-serially by the finalize, so results stay exact), kStrLongs = long
-// records listed.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kStrErr = 0;
-constexpr uint32_t kStrLongs = 1;
-constexpr uint32_t kStrLongChunks = 64;  // more interior chunks: stream_long_kernel
-
-struct StreamGeom
-{
-    uint64_t c_first;  // first chunk index (absolute address / 4096)
-    uint32_t nchunks;
-};
-
-__device__ __forceinline__ StreamGeom stream_geom(const uint8_t* base, const uint64_t* off,
-                                                  uint64_t span)
-{
-    const uint64_t lo = uint64_t(base) + off[0];
-    StreamGeom g;
-    g.c_first = lo / kChunk;
-    g.nchunks = uint32_t((lo + (span ? span : 1) - 1) / kChunk - g.c_first + 1);
-    return g;
-}
-
-// End point 2i + 1 duplicates start point 2i + 2.
-__device__ __forceinline__ bool end_is_next_start(const uint64_t* off, const uint32_t* len,
-                                                  uint64_t count, uint64_t i)
-{
-    return i + 1 < count && off[i + 1] == off[i] + len[i];
-}
-
-// One thread per record: checks the order, marks the rows of the record's
-// start and end in their chunks' row masks.  Row 0 needs no snapshot (the
-// chains are zero there) and chunk starts need no prefix at all, so neither
-// is marked.
-__global__ __launch_bounds__(256) void stream_mark_kernel(const uint8_t* __restrict__ base,
-                                                          const uint64_t* __restrict__ off,
-                                                          const uint32_t* __restrict__ len,
-                                                          uint64_t count, uint64_t span,
-                                                          uint32_t* __restrict__ masks,
-                                                          uint32_t* __restrict__ ctrl)
-{
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const StreamGeom g = stream_geom(base, off, span);
-    const uint64_t o = off[i], E = o + len[i];
-    const bool ordered = i + 1 < count ? off[i + 1] >= E && E >= o : E <= off[0] + span && E >= o;
-    if (!ordered) atomicOr(ctrl + kStrErr, 1u);
-    auto mark = [&](uint64_t a) {
-        const uint64_t x = a - g.c_first * kChunk;
-        const uint32_t row = uint32_t(x % kChunk) / kRowBytes;
-        if (row != 0 && x / kChunk < g.nchunks) atomicOr(masks + x / kChunk, 1u << row);
-    };
-    mark(uint64_t(base) + o);
-    if (!end_is_next_start(off, len, count, i)) mark(uint64_t(base) + E);
-}
-
-// The chunk pass: the headline kernel's row ring over chunks k = 0 ..
-// nchunks - 1 of the stream (team t takes chunks t, t + nteams, ...), raw
-// registers (no init) into R[k], and before every marked row the team's
-// chain registers into snaps[(k * 32 + row) * 8 + lane] (16 B per lane).  A
-// wave's 8 teams take 8 consecutive chunks: their masks are read with scalar
-// loads and OR-ed, so a row no team of the wave marks costs two scalar
-// instructions.
-__global__ __launch_bounds__(kBlock, 1) void crc32c_stream_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off, uint64_t span,
-    const uint32_t* __restrict__ masks, uint32_t* __restrict__ R, uint4* __restrict__ snaps,
-    const uint32_t* __restrict__ ctrl, const uint32_t* __restrict__ tables)
-{
-    constexpr int NB = 4, AHEAD = NB - 1, RR = 32;
-    // records out of order: [lo, lo + span) is not known to be readable
-    if (ctrl[kStrErr]) return;
-    stage_tables(tables);
-    const StreamGeom g = stream_geom(base, off, span);
-    const uint32_t tl = threadIdx.x & (kTeam - 1);
-    const uint32_t li = lane_info();
-    const uint32_t team = (blockIdx.x * kBlock + threadIdx.x) / kTeam;
-    const uint32_t nteams = gridDim.x * kBlock / kTeam;
-    const uint32_t team0 = __builtin_amdgcn_readfirstlane(team & ~7u);  // the wave's first team
-    const uint32_t count = g.nchunks;
-    const uint32_t iters = team0 < count ? (count - team0 + nteams - 1) / nteams : 0;
-    if (iters == 0) return;
-    const uint8_t* c0 = reinterpret_cast<const uint8_t*>(g.c_first * kChunk);
-    auto chunk_of = [&](uint32_t it) {
-        const uint32_t k = team + it * nteams;
-        return k < count ? k : count - 1;
-    };
-    auto wave_mask = [&](uint32_t it) {
-        const uint32_t kb = team0 + it * nteams;  // uniform: scalar loads
-        uint32_t w = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) w |= kb + j < count ? masks[kb + j] : 0u;
-        return w;
-    };
-    auto row_ptr = [&](uint32_t k, int r) { return c0 + uint64_t(k) * kChunk + tl * 16 + r * kRowBytes; };
-
-    uint4 buf[NB];
-    uint32_t k = chunk_of(0);
-    // row masks one chunk ahead (their latency hides behind a chunk's rows)
-    uint32_t wm = wave_mask(0), m = masks[k];
-#pragma unroll
-    for (int r = 0; r < AHEAD; ++r) buf[r] = load16(row_ptr(k, r));
-    for (uint32_t it = 0; it < iters; ++it)
-    {
-        const uint32_t kn = chunk_of(it + 1);
-        const uint32_t wm_next = wave_mask(it + 1), m_next = masks[kn];
-        uint4* snap = snaps + (uint64_t(k) * RR) * kTeam + tl;
-        uint32_t V[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int r = 0; r < RR; ++r)
-        {
-            const int ra = r + AHEAD;
-            buf[ra % NB] = load16(ra < RR ? row_ptr(k, ra) : row_ptr(kn, ra - RR));
-            __builtin_amdgcn_sched_barrier(0);
-            if (r != 0 && (wm >> r) & 1u)  // wave-uniform
-            {
-                if ((m >> r) & 1u) snap[r * kTeam] = make_uint4(V[0], V[1], V[2], V[3]);
-            }
-            if (MI_FIRST_ROW_COPY && r == 0)
-                row_first(V, buf[0]);
-            else
-                row_update(V, buf[r % NB], li);
-        }
-        const uint32_t raw = team_fold(V);
-        if (tl == 0 && team + it * nteams < count) R[k] = raw;
-        k = kn;
-        wm = wm_next;
-        m = m_next;
-    }
-}
-
-// One team per boundary point q (record q / 2; its start, or for odd q its
-// end) that is not on a chunk start and not a duplicate: P = raw(chunk[0,
-// x)) from the snapshot of the point's row (zero for row 0) and the row
-// itself, masked to the bytes before x:
-//   W = Z_128(V) ^ masked row;  fold(W) = Z_m(P), m = 128 (row + 1) - x.
-__global__ __launch_bounds__(kBlock, 1) void stream_points_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, uint64_t count, uint64_t span,
-    const uint4* __restrict__ snaps, uint32_t* __restrict__ pval,
-    const uint32_t* __restrict__ ctrl, const uint32_t* __restrict__ tables)
-{
-    if (ctrl[kStrErr]) return;  // out of order: the finalize hashes byte-serially
-    stage_tables(tables);
-    const StreamGeom g = stream_geom(base, off, span);
-    const uint32_t tl = threadIdx.x & (kTeam - 1);
-    const uint32_t li = lane_info();
-    const uint64_t team = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kTeam;
-    const uint64_t nteams = uint64_t(gridDim.x) * kBlock / kTeam;
-    const uint64_t rel = uint64_t(base) - g.c_first * kChunk;  // chunk-relative = rel + offset
-    // Point q of this team (q = 2i start, 2i + 1 end) -> its inputs, loaded
-    // one point ahead: chunk-relative position, snapshot, row.
-    struct In
-    {
-        uint64_t x;
-        uint4 v, d;
-        bool live;
-    };
-    // the team's points: q = team + j * nteams over [0, 2 count), skipping
-    // ends that repeat the next start or close empty records
-    auto pos_of = [&](uint64_t q, bool* live) {
-        const uint64_t i = q >> 1;
-        const bool is_end = q & 1u;
-        const uint64_t o = off[i];
-        const uint32_t L = len[i];
-        const uint64_t x = rel + o + (is_end ? L : 0u);
-        *live = (x % kChunk) != 0 &&
-                !(is_end && (L == 0 || (i + 1 < count && off[i + 1] == o + L)));
-        return x;
-    };
-    auto fetch = [&](uint64_t q, In& in) {
-        in.x = pos_of(q, &in.live);
-        const uint32_t xc = uint32_t(in.x % kChunk), row = xc / kRowBytes;
-        const uint64_t k = in.x / kChunk;
-        // dead points (an end point may lie one chunk past the stream) read
-        // the zero block and no snapshot
-        const uint8_t* rp = in.live ? reinterpret_cast<const uint8_t*>((g.c_first + k) * kChunk) +
-                                          row * kRowBytes + tl * 16
-                                    : reinterpret_cast<const uint8_t*>(tables + kTabZero);
-        in.d = load16(rp);
-        in.v = in.live && row != 0 ? snaps[(k * 32 + row) * kTeam + tl] : make_uint4(0, 0, 0, 0);
-    };
-    const uint64_t npts = 2 * count;
-    if (team >= npts) return;
-    In cur, nxt;
-    fetch(team, cur);
-    for (uint64_t q = team; q < npts; q += nteams)
-    {
-        const uint64_t qn = q + nteams < npts ? q + nteams : q;
-        fetch(qn, nxt);
-        if (cur.live)  // uniform over the team
-        {
-            const uint32_t xc = uint32_t(cur.x % kChunk);
-            uint32_t V[4] = {cur.v.x, cur.v.y, cur.v.z, cur.v.w};
-            const uint4 d = mask_below(cur.d, int32_t(xc % kRowBytes) - int32_t(tl) * 16);
-            row_update(V, d, li);
-            const uint32_t F = team_fold(V);
-            if (tl == 0)
-            {
-                const uint32_t mneg = kRowBytes - xc % kRowBytes;  // 1 .. 128
-                pval[q] = mneg == kRowBytes ? zglob(tables + kTabZInv128, F)
-                                            : zglob(tables + kTabZNeg + mneg * 1024, F);
-            }
-        }
-        cur = nxt;
-    }
-}
-
-// Z_n, 0 <= n <= 4096, through G^{2^b}, b = 0..12, staged in LDS.
-__device__ __forceinline__ uint32_t zsmall(const uint32_t (*p2)[1024], uint32_t v, uint32_t n)
-{
-#pragma unroll
-    for (int b = 0; b < 13; ++b)
-        if ((n >> b) & 1u) v = zglob(p2[b], v);
-    return v;
-}
-
-// Prefix registers at record i's start and end (chunk-relative a, E).
-__device__ __forceinline__ void record_prefixes(const uint64_t* off, const uint32_t* len,
-                                                uint64_t count, uint64_t i, uint32_t xa,
-                                                uint32_t xe, uint64_t k1, const uint32_t* R,
-                                                const uint32_t* pval, uint32_t* pa, uint32_t* pe)
-{
-    *pa = xa ? pval[2 * i] : 0u;
-    *pe = xe == kChunk ? R[k1] : pval[end_is_next_start(off, len, count, i) ? 2 * i + 2 : 2 * i + 1];
-}
-
-// One thread per record (see the section comment); records with more than
-// kStrLongChunks interior chunks are listed for stream_long_kernel.
-__global__ __launch_bounds__(512) void stream_finalize_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
-    uint64_t span, const uint32_t* __restrict__ R, const uint32_t* __restrict__ pval,
-    uint32_t* __restrict__ ctrl, uint32_t* __restrict__ longs, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables)
-{
-    __shared__ uint32_t p2[13][1024];  // G^{2^b}: Z_1 .. Z_4096
-    __shared__ uint32_t t0[256];
-    for (uint32_t i = threadIdx.x; i < 13 * 1024; i += blockDim.x) p2[i >> 10][i & 1023] = tables[kTabP2 + i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) t0[i] = tables[kTabT + i];
-    __syncthreads();
-    const bool err = ctrl[kStrErr] != 0;
-    const StreamGeom g = stream_geom(base, off, span);
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
-         i += uint64_t(gridDim.x) * blockDim.x)
-    {
-        const uint32_t L = len[i];
-        const uint32_t init = inits ? inits[i] : 0u;
-        if (L == 0)
-        {
-            out[i] = init;
-            continue;
-        }
-        if (err)  // the records are not in order: exact, slowly
-        {
-            const uint8_t* q = base + off[i];
-            uint32_t c = ~init;
-            for (uint32_t j = 0; j < L; ++j) c = t0[(c ^ q[j]) & 0xFFu] ^ (c >> 8);
-            out[i] = ~c;
-            continue;
-        }
-        const uint64_t a = uint64_t(base) + off[i] - g.c_first * kChunk, E = a + L;
-        const uint64_t k0 = a / kChunk, k1 = (E - 1) / kChunk;
-        const uint32_t xa = uint32_t(a % kChunk), xe = uint32_t(E - k1 * kChunk);
-        if (k1 > k0 + 1 + kStrLongChunks)
-        {
-            longs[atomicAdd(ctrl + kStrLongs, 1u)] = uint32_t(i);
-            continue;
-        }
-        uint32_t pa, pe;
-        record_prefixes(off, len, count, i, xa, xe, k1, R, pval, &pa, &pe);
-        uint32_t s = ~init ^ pa;
-        if (k0 == k1)
-            s = zsmall(p2, s, xe - xa) ^ pe;
-        else
-        {
-            s = zsmall(p2, s, kChunk - xa) ^ R[k0];
-            for (uint64_t k = k0 + 1; k < k1; ++k) s = zglob(p2[12], s) ^ R[k];
-            s = zsmall(p2, s, xe) ^ pe;
-        }
-        out[i] = ~s;
-    }
-}
-
-// Records with more than kStrLongChunks interior chunks, one workgroup each:
-// thread t folds interior chunks jj = t + 1024 q (counted from the record's
-// last interior chunk) by Horner with Z_{1024 * 4096}, shifts by Z_{4096 t}
-// and the workgroup XOR-reduces; thread 0 joins the head and the tail.
-__global__ __launch_bounds__(kLongBlock) void stream_long_kernel(
-    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
-    uint64_t span, const uint32_t* __restrict__ R, const uint32_t* __restrict__ pval,
-    const uint32_t* __restrict__ ctrl, const uint32_t* __restrict__ longs,
-    uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
-    const uint32_t* __restrict__ pow2)
-{
-    __shared__ uint32_t zs[1024];
-    __shared__ uint32_t zc2[10][1024];
-    __shared__ uint32_t red[kLongBlock / 64];
-    if (ctrl[kStrErr]) return;
-    const uint32_t nlong = ctrl[kStrLongs];
-    if (blockIdx.x >= nlong) return;
-    for (uint32_t i = threadIdx.x; i < 1024; i += kLongBlock) zs[i] = tables[kTabZLong + i];
-    for (uint32_t i = threadIdx.x; i < 10 * 1024; i += kLongBlock)
-        zc2[i / 1024][i % 1024] = tables[kTabZC2 + i];
-    __syncthreads();
-    const StreamGeom g = stream_geom(base, off, span);
-    const uint32_t t = threadIdx.x;
-    auto zbig = [&](uint32_t v, uint64_t n) {
-        for (int b = 0; n && b < 48; ++b, n >>= 1)
-            if (n & 1u) v = zglob(pow2 + b * 1024, v);
-        return v;
-    };
-    for (uint32_t q = blockIdx.x; q < nlong; q += gridDim.x)
-    {
-        const uint32_t i = longs[q];
-        const uint32_t L = len[i];
-        const uint64_t a = uint64_t(base) + off[i] - g.c_first * kChunk, E = a + L;
-        const uint64_t k0 = a / kChunk, k1 = (E - 1) / kChunk;
-        const uint64_t nint = k1 - k0 - 1;
-        uint32_t acc = 0;
-        if (t < nint)
-        {
-            const uint64_t n_t = (nint - t + kLongBlock - 1) / kLongBlock;
-            for (uint64_t j = n_t; j-- > 0;) acc = zglob(zs, acc) ^ R[k1 - 1 - (t + j * kLongBlock)];
-            for (int b = 0; b < 10; ++b)
-                if (t & (1u << b)) acc = zglob(zc2[b], acc);
-        }
-        for (int d = 32; d >= 1; d >>= 1) acc ^= __shfl_xor(acc, d);
-        if ((t & 63) == 0) red[t >> 6] = acc;
-        __syncthreads();
-        if (t == 0)
-        {
-            uint32_t c = 0;
-            for (int w = 0; w < kLongBlock / 64; ++w) c ^= red[w];
-            const uint32_t xa = uint32_t(a % kChunk), xe = uint32_t(E - k1 * kChunk);
-            uint32_t pa, pe;
-            record_prefixes(off, len, count, i, xa, xe, k1, R, pval, &pa, &pe);
-            uint32_t h = zbig(~(inits ? inits[i] : 0u) ^ pa, kChunk - xa) ^ R[k0];
-            h = zbig(h, nint * kChunk) ^ c;  // across the interior run
-            out[i] = ~(zbig(h, xe) ^ pe);
-        }
-        __syncthreads();
-    }
-}
-
-uint64_t stream_max_chunks(uint64_t span) { return span / kChunk + 2; }
-
-hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32_t* lengths,
-                         const uint32_t* inits, uint64_t count, uint64_t span,
-                         const StreamWorkspace& ws, uint32_t* out, const uint32_t* tables,
-                         const uint32_t* pow2, int cus, hipStream_t stream)
-{
-    if (count == 0) return hipSuccess;
-    const uint8_t* b = static_cast<const uint8_t*>(base);
-    const uint64_t maxc = stream_max_chunks(span);
-    hipError_t e = hipMemsetAsync(ws.ctrl, 0, kStreamCtrlWords * 4 + maxc * 4, stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(stream_mark_kernel, dim3(uint32_t((count + 255) / 256)), dim3(256), 0,
-                       stream, b, offsets, lengths, count, span, ws.masks, ws.ctrl);
-    const uint64_t need = (maxc + (kBlock / kTeam) - 1) / (kBlock / kTeam);
-    const int grid = int(std::min<uint64_t>(uint64_t(cus), std::max<uint64_t>(need, 1)));
-    hipLaunchKernelGGL(crc32c_stream_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream, b,
-                       offsets, span, ws.masks, ws.R, ws.snaps, ws.ctrl, tables);
-    const uint64_t pneed = (2 * count + (kBlock / kTeam) - 1) / (kBlock / kTeam);
-    const int pgrid = int(std::min<uint64_t>(uint64_t(cus), std::max<uint64_t>(pneed, 1)));
-    hipLaunchKernelGGL(stream_points_kernel, dim3(pgrid), dim3(kBlock), kLdsBytes, stream, b,
-                       offsets, lengths, count, span, ws.snaps, ws.pval, ws.ctrl, tables);
-    const uint64_t fin_blocks = (count + 511) / 512;
-    hipLaunchKernelGGL(stream_finalize_kernel, dim3(uint32_t(fin_blocks < 1024 ? fin_blocks : 1024)),
-                       dim3(512), 0, stream, b, offsets, lengths, inits, count, span, ws.R,
-                       ws.pval, ws.ctrl, ws.longs, out, tables);
-    const uint32_t lgrid = uint32_t(count < 256 ? count : 256);
-    hipLaunchKernelGGL(stream_long_kernel, dim3(lgrid), dim3(kLongBlock), 0, stream, b, offsets,
-                       lengths, inits, count, span, ws.R, ws.pval, ws.ctrl, ws.longs, out, tables,
-                       pow2);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // Variable-length batches, sorted path: one team per
 // whole record, records binned by row count inside each workgroup's share.
 //   sorted_cost_kernel:   per block of 1,024 records, the sum of the records'
@@ -2300,39 +1740,9 @@ hipError_t launch_stream(const void* base, const uint64_t* offsets, const uint32
 constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
 constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 1;  // rows of the largest item (513)
 constexpr uint32_t kSortBins = kSortRows;                         // bin = kSortRows - rows
-#ifndef MI_SORT_FOLD
-#define MI_SORT_FOLD 2
-#endif
 // rows per ring of the sorted kernel (2 or 4)
 #ifndef MI_SORT_RING
 #define MI_SORT_RING 2
-#endif
-// measurement knob: groups grabbed from a per-workgroup counter in global
-// memory (256-B spaced, zeroed by sorted_cost_kernel) instead of LDS: the
-// owner-side cost of any cross-workgroup stealing scheme
-#ifndef MI_SORT_GGRAB
-#define MI_SORT_GGRAB 0
-#endif
-constexpr uint32_t kSortWgcBase = 64, kSortWgcStride = 64;  // ctrl words
-// measurement knob: descriptors read with non-temporal loads
-#ifndef MI_SORT_NTDLOAD
-#define MI_SORT_NTDLOAD 0
-#endif
-// measurement knob: the CRCs written with non-temporal stores
-#ifndef MI_SORT_NTOUT
-#define MI_SORT_NTOUT 0
-#endif
-// descriptors written with non-temporal stores (see place)
-#ifndef MI_SORT_NTDESC
-#define MI_SORT_NTDESC 1
-#endif
-// 2-row groups: the last row issued at the group's start (see step)
-#ifndef MI_SORT_SHORTPRE
-#define MI_SORT_SHORTPRE 1
-#endif
-// group loop unrolled twice with the current/next views swapped (no copies)
-#ifndef MI_SORT_PINGPONG
-#define MI_SORT_PINGPONG 1
 #endif
 // XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
 // and in every timeline measured (tools/sorted_stamps.py, 5 GPU sessions)
@@ -2340,10 +1750,8 @@ constexpr uint32_t kSortWgcBase = 64, kSortWgcStride = 64;  // ctrl words
 // shares.  Even workgroups take MI_SORT_XCDW/1000 more cost, odd ones as much
 // less (A/B against equal shares: 0.878-0.905 ms vs 0.885-0.916 at 20;
 // 15 is the default, 0 turns it off).
-#ifndef MI_SORT_XCDW
-#define MI_SORT_XCDW 15
-#endif
-constexpr uint32_t kSortFold = MI_SORT_FOLD;  // cost allowance per item, in rows (fold, masks)
+constexpr uint32_t kSortXcdw = 15;
+constexpr uint32_t kSortFold = 2;            // cost allowance per item, in rows (fold, masks)
 constexpr uint32_t kSortPer = 1;             // records per thread of a cost block
 constexpr uint32_t kSortRecs = kPlanThreads * kSortPer;
 constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a split record
@@ -2359,13 +1767,6 @@ constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
 // (tools/sorted_stamps.py)
 #ifndef MI_SORT_STAMP
 #define MI_SORT_STAMP 0
-#endif
-// measurement builds only (tools/build_variant.sh, tools/stop_probe.sh),
-// results are wrong: stop after the descriptors (1), the block search (2),
-// the boundaries (3), the table staging (4), binning pass 1 (5), the bin
-// scan and item allocation (6): times the prologue's phases
-#ifndef MI_SORT_STOP
-#define MI_SORT_STOP 0
 #endif
 
 uint32_t sorted_blocks(uint64_t count) { return uint32_t((count + kSortRecs - 1) / kSortRecs); }
@@ -2399,19 +1800,17 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
     return uint64_t(lo) | (uint64_t(hi) << 32);
 }
 
-// Cost blocks per launch block (MI_SORT_COSTX): thread t of block j takes
-// record t of cost blocks X j .. X j + X - 1, all loads issued first.
-#ifndef MI_SORT_COSTX
-#define MI_SORT_COSTX 1
-#endif
+// Two or four cost blocks per launch block, every load issued first, gave
+// kernel minimums of 6.2 and 6.5 us against 7.2 but did not move the step
+// (5 interleaved rounds, profiles/r02_sorted_cost_kernel_ab.txt).
 __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     uint64_t* __restrict__ blk_cost, uint32_t* __restrict__ ctrl, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables, uint32_t nwg)
+    const uint32_t* __restrict__ tables)
 {
     static_assert(kSortPer == 1, "one record per thread and cost block");
-    constexpr uint32_t X = MI_SORT_COSTX;
+    constexpr uint32_t X = 1;
     __shared__ uint64_t sh[X][kPlanThreads / 64];
     uint64_t av[X];
     uint32_t Lv[X];
@@ -2461,10 +1860,6 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
         ctrl[0] = 0;  // item allocation cursor
         ctrl[1] = 0;  // overflow flag
     }
-    if (MI_SORT_GGRAB)
-        for (uint64_t w = uint64_t(blockIdx.x) * kPlanThreads + threadIdx.x; w < nwg;
-             w += uint64_t(gridDim.x) * kPlanThreads)
-            ctrl[kSortWgcBase + w * kSortWgcStride] = 0;
 }
 
 // LDS of the sorted kernel beyond the table image.
@@ -2544,12 +1939,12 @@ __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ bl
     uint64_t T[2];
     T[0] = tot / G * b + (tot % G) * b / G;
     T[1] = b + 1 == G ? tot : tot / G * (b + 1) + (tot % G) * (b + 1) / G;
-    if (MI_SORT_XCDW && !(G & 1))
+    if (kSortXcdw && !(G & 1))
     {
         // T(x) = C (1000 x + w (x & 1)) / (1000 G): share 1 + w/1000 for even
         // b, 1 - w/1000 for odd b; T(G) = C exactly
         auto at = [&](uint64_t x) {
-            return x >= G ? tot : uint64_t(double(tot) * (double(x) * 1000.0 + MI_SORT_XCDW * double(x & 1)) /
+            return x >= G ? tot : uint64_t(double(tot) * (double(x) * 1000.0 + kSortXcdw * double(x & 1)) /
                                            (double(G) * 1000.0));
         };
         T[0] = at(b);
@@ -2681,75 +2076,42 @@ __device__ __forceinline__ uint32_t init_dword(uint32_t ninit, int32_t q, int k)
 
 // The masks depend on the record's init, loaded here and consumed a group
 // later (sort_view runs for the NEXT group), so the load costs no wait.
-#ifndef MI_SORT_VIEW32
-#define MI_SORT_VIEW32 1
-#endif
+// 32-bit window arithmetic (an item spans < 2^17 bytes); one 64-bit add for
+// the row pointer.  The init word: (hi:lo) = ~init << 8 (q & 3) goes to
+// dwords q>>2 and q>>2 + 1 of the lane's block (q = the record's first byte
+// there, -3..15), or to row f + 1 (lane 0, q >= 125).  (Against five 64-bit
+// shifts per view: SQ_INSTS_VALU -9 % on the < 256 B class.)
 __device__ __forceinline__ SortView sort_view(const uint4& d, int32_t n, uint32_t tl,
                                               const uint32_t* __restrict__ inits,
                                               const uint32_t* __restrict__ zero_word,
                                               const uint32_t* __restrict__ ones_word)
 {
     SortView v;
-#if MI_SORT_VIEW32
-    // 32-bit window arithmetic (an item spans < 2^17 bytes); one 64-bit add
-    // for the row pointer.  The init word: (hi:lo) = ~init << 8 (q & 3) goes
-    // to dwords q>>2 and q>>2 + 1 of the lane's block (q = the record's
-    // first byte there, -3..15), or to row f + 1 (lane 0, q >= 125).
-    {
-        const uint32_t L = d.z;
-        const int32_t s0 = int32_t(d.x & (kRowBytes - 1));
-        const int32_t se = s0 + int32_t(L);
-        const int32_t rows = L ? (se + int32_t(kRowBytes) - 1) >> 7 : 0;
-        v.recf = L ? d.w : kSortNone;
-        v.f = n - rows;
-        const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
-        v.p0 = ps + int64_t(int32_t(uint32_t(rows - n) * kRowBytes + tl * 16u) - s0);
-        const int32_t q = s0 - int32_t(tl) * 16;
-        const int32_t bs = min(max(q, 0), 16);
-        const int32_t ce = min(max(se - (rows - 1) * int32_t(kRowBytes) - int32_t(tl) * 16, 0), 16);
-        v.lo = L ? v.f + (bs >= 16 ? 1 : 0) : n;
-        v.hi = L ? n - 1 - (ce == 0 ? 1 : 0) : -1;
-        v.m = uint32_t(rows * int32_t(kRowBytes) - se);
-        v.kf = make_uint4(keep_from(bs, 0), keep_from(bs, 1), keep_from(bs, 2), keep_from(bs, 3));
-        v.ke = make_uint4(keep_below(ce, 0), keep_below(ce, 1), keep_below(ce, 2), keep_below(ce, 3));
-        const bool with_init = L && (!(d.w & kSortMulti) || (d.w & kSortFirst));
-        const uint32_t ninit = ~*(!with_init ? ones_word : inits ? inits + (d.w & kSortRecMask) : zero_word);
-        const uint64_t sh = uint64_t(ninit) << ((uint32_t(q) & 3u) * 8u);
-        const uint32_t xl = uint32_t(sh), xh = uint32_t(sh >> 32);
-        const int32_t qd = q >> 2;  // arithmetic: -1 for q in -3..-1
-        v.xf = make_uint4(qd == 0 ? xl : qd == -1 ? xh : 0u, qd == 1 ? xl : qd == 0 ? xh : 0u,
-                          qd == 2 ? xl : qd == 1 ? xh : 0u, qd == 3 ? xl : qd == 2 ? xh : 0u);
-        v.xs = q >= int32_t(kRowBytes) - 3 ? xh : 0u;
-        return v;
-    }
-#endif
-    const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
-    const uint64_t E = ps + d.z;
-    const uint64_t w0 = ps & ~uint64_t(kRowBytes - 1), w1 = (E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
-    const int32_t rows = int32_t(sort_rows(d));
-    v.recf = d.z ? d.w : kSortNone;
+    const uint32_t L = d.z;
+    const int32_t s0 = int32_t(d.x & (kRowBytes - 1));
+    const int32_t se = s0 + int32_t(L);
+    const int32_t rows = L ? (se + int32_t(kRowBytes) - 1) >> 7 : 0;
+    v.recf = L ? d.w : kSortNone;
     v.f = n - rows;
-    v.p0 = w1 - uint64_t(n) * kRowBytes + tl * 16u;
-    const int32_t s0 = int32_t(ps - w0);
-    const int32_t bs = min(max(s0 - int32_t(tl) * 16, 0), 16);
-    v.lo = v.f + (bs >= 16 ? 1 : 0);
-    const int32_t ce = min(max(int32_t(E - (w1 - kRowBytes)) - int32_t(tl) * 16, 0), 16);
-    v.hi = n - 1 - (ce == 0 ? 1 : 0);
-    if (!d.z)
-    {
-        v.lo = n;
-        v.hi = -1;
-    }
-    v.m = uint32_t(w1 - E);
+    const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
+    v.p0 = ps + int64_t(int32_t(uint32_t(rows - n) * kRowBytes + tl * 16u) - s0);
+    const int32_t q = s0 - int32_t(tl) * 16;
+    const int32_t bs = min(max(q, 0), 16);
+    const int32_t ce = min(max(se - (rows - 1) * int32_t(kRowBytes) - int32_t(tl) * 16, 0), 16);
+    v.lo = L ? v.f + (bs >= 16 ? 1 : 0) : n;
+    v.hi = L ? n - 1 - (ce == 0 ? 1 : 0) : -1;
+    v.m = uint32_t(rows * int32_t(kRowBytes) - se);
     v.kf = make_uint4(keep_from(bs, 0), keep_from(bs, 1), keep_from(bs, 2), keep_from(bs, 3));
     v.ke = make_uint4(keep_below(ce, 0), keep_below(ce, 1), keep_below(ce, 2), keep_below(ce, 3));
-    const bool with_init = d.z && (!(d.w & kSortMulti) || (d.w & kSortFirst));
+    const bool with_init = L && (!(d.w & kSortMulti) || (d.w & kSortFirst));
     // always one load (0 without inits, all ones where no init word goes in)
     const uint32_t ninit = ~*(!with_init ? ones_word : inits ? inits + (d.w & kSortRecMask) : zero_word);
-    const int32_t q = s0 - int32_t(tl) * 16;  // the record's first byte in this lane's block of row f
-    v.xf = make_uint4(init_dword(ninit, q, 0), init_dword(ninit, q, 1), init_dword(ninit, q, 2),
-                      init_dword(ninit, q, 3));
-    v.xs = init_dword(ninit, q - int32_t(kRowBytes), 0);  // lane 0 of row f + 1, when s0 > 124
+    const uint64_t sh = uint64_t(ninit) << ((uint32_t(q) & 3u) * 8u);
+    const uint32_t xl = uint32_t(sh), xh = uint32_t(sh >> 32);
+    const int32_t qd = q >> 2;  // arithmetic: -1 for q in -3..-1
+    v.xf = make_uint4(qd == 0 ? xl : qd == -1 ? xh : 0u, qd == 1 ? xl : qd == 0 ? xh : 0u,
+                      qd == 2 ? xl : qd == 1 ? xh : 0u, qd == 3 ? xl : qd == 2 ? xh : 0u);
+    v.xs = q >= int32_t(kRowBytes) - 3 ? xh : 0u;
     return v;
 }
 
@@ -2782,17 +2144,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x == 0) S.next_group = 0;
     stage_tables(tables);  // ends with a barrier
     if (MI_SORT_STAMP && lane == 0) stamps[3] = __builtin_amdgcn_s_memrealtime();
-    if (MI_SORT_STOP == 4) return;
 
     // (1) Wave 0: the two targets and the cost blocks holding them.
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
     if (MI_SORT_STAMP && lane == 0) stamps[4] = __builtin_amdgcn_s_memrealtime();
-    if (MI_SORT_STOP == 2) return;
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S);
     if (MI_SORT_STAMP && lane == 0) stamps[5] = __builtin_amdgcn_s_memrealtime();
-    if (MI_SORT_STOP == 3) return;
 
     // (3) Bin the items by row count, largest first.  Whole records and the
     // last pieces of split records go to this workgroup's slots of the
@@ -2844,15 +2203,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint4* const fullv = items + count;
     uint4* const lastv = items + rlo;
     // absolute slots: full run at fpos, last piece at lpos
-    // Descriptors go out with non-temporal stores (MI_SORT_NTDESC): the
-    // ~2 MB of them per XCD then do not sit dirty in the XCD's 4 MB L2
-    // through the hash phase (measured: prologue 8 us longer, step 8-10 us
-    // shorter).  The group loop reads them two groups ahead.
+    // Descriptors go out with non-temporal stores: the ~2 MB of them per XCD
+    // then do not sit dirty in the XCD's 4 MB L2 through the hash phase
+    // (measured: prologue 8 us longer, step 8-10 us shorter).  The group loop
+    // reads them two groups ahead (non-temporal loads there: neutral).
     auto put = [&](uint4* dst, const uint4& dv) {
-        if (MI_SORT_NTDESC)
-            __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
-        else
-            *dst = dv;
+        __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
     };
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
         for (uint32_t i = 0; i < f.nf; ++i) put(fullv + S.full_base + fpos + i, desc(r, a, L, f, f.klo + i));
@@ -2899,7 +2255,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     pass(false);
     __syncthreads();
     if (MI_SORT_STAMP == 1 && lane == 0) stamps[6] = __builtin_amdgcn_s_memrealtime();
-    if (MI_SORT_STOP == 5) return;
     {
         const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
         uint64_t total;
@@ -2928,7 +2283,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     __syncthreads();
     if (MI_SORT_STAMP == 1 && lane == 0) stamps[7] = __builtin_amdgcn_s_memrealtime();
-    if (MI_SORT_STOP == 6) return;
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     if (n_items)
     {
@@ -2954,7 +2308,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             pass(true);
     }
     __syncthreads();
-    if (n_items == 0 || MI_SORT_STOP == 1) return;
+    if (n_items == 0) return;
 
     if (MI_SORT_STAMP && lane == 0) stamps[1] = __builtin_amdgcn_s_memrealtime();
     // (4) Groups of 8 items, largest first, one LDS grab per group.
@@ -2981,12 +2335,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             const uint32_t rec = p_recf & kSortRecMask;
             if (!(p_recf & kSortMulti))
-            {
-                if (MI_SORT_NTOUT)
-                    __builtin_nontemporal_store(~v, out + rec);
-                else
-                    out[rec] = ~v;
-            }
+                out[rec] = ~v;  // (non-temporal stores here: slower, partial lines)
             else
             {
                 // this piece's part: Z_{E - pe}(raw(piece)), E the record's end
@@ -2998,14 +2347,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     auto grab = [&]() {
         uint32_t g = 0;
-        if (MI_SORT_GGRAB)
-        {
-            if (lane == 0)
-                g = __hip_atomic_fetch_add(ctrl + kSortWgcBase + uint64_t(blockIdx.x) * kSortWgcStride,
-                                           1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        else if (lane == 0)
-            g = atomicAdd(&S.next_group, 1u);
+        if (lane == 0) g = atomicAdd(&S.next_group, 1u);
         return uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
     };
     const uint4* const listF = items + count + S.full_base;  // full pieces first
@@ -3014,8 +2356,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const uint32_t i = g * 8 + tw;
         const uint4* p = (g < n_groups && i < n_items) ? (i < n_full ? listF : listL) + i
                                                        : reinterpret_cast<const uint4*>(zero16);
-        // MI_SORT_NTDLOAD: read once, so a non-temporal load
-        return MI_SORT_NTDLOAD ? load16(reinterpret_cast<const uint8_t*>(p)) : *p;
+        return *p;
     };
     // Uniform shape of a group: n rows (its largest item, padded to an even
     // count with a leading zero row), the first row of that item, the last
@@ -3083,7 +2424,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         // A 2-row group runs no body loop, so its last row can be issued now,
         // a whole group header ahead of its folding, instead of one row
         // ahead (MI_SORT_SHORTPRE); b[1] is free here.
-        const bool pre = MI_SORT_SHORTPRE && RB == 2 && sh.n == 2;
+        const bool pre = RB == 2 && sh.n == 2;
         if (pre) b[1] = load16(row_ptr(cur, 1, false));
         const uint32_t g_nn = grab();
         const uint4 d_nn = load_desc(g_nn);
@@ -3180,21 +2521,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         g_nxt = g_nn;
         d_nxt = d_nn;
     };
-#if MI_SORT_PINGPONG
+    // twice per iteration with the two views swapped: the ~20 registers of a
+    // view are never copied at the back edge (~60 v_mov per group before)
     while (shA.n > 0)
     {
         step(vA, shA, vB, shB);
         if (shB.n <= 0) break;
         step(vB, shB, vA, shA);
     }
-#else
-    while (shA.n > 0)
-    {
-        step(vA, shA, vB, shB);
-        vA = vB;
-        shA = shB;
-    }
-#endif
     flush();
     if (MI_SORT_STAMP && lane == 0) stamps[2] = __builtin_amdgcn_s_memrealtime();
 }
@@ -3207,9 +2541,8 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     if (count == 0) return hipSuccess;
     const uint32_t nb = sorted_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
-    hipLaunchKernelGGL(sorted_cost_kernel, dim3((nb + MI_SORT_COSTX - 1) / MI_SORT_COSTX),
-                       dim3(kPlanThreads), 0, stream, b, offsets,
-                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, uint32_t(grid));
+    hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
+                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables);
     hipLaunchKernelGGL(crc32c_sorted_kernel, dim3(grid), dim3(kBlock), kLdsSorted, stream, b,
                        offsets, lengths, inits, count, ws.blk_cost, nb, ws.ctrl, ws.items,
                        ws.item_cap, out, tables, pow2);
@@ -3243,10 +2576,6 @@ hipError_t configure_kernels()
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_direct_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    for (const void* f : {reinterpret_cast<const void*>(&crc32c_stream_kernel),
-                          reinterpret_cast<const void*>(&stream_points_kernel)})
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);

@@ -303,7 +303,6 @@ struct Ctx
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
-    DevBuf s_ctrl, s_R, s_snaps, s_pval;  // stream path (sorted batches)
     DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
     PinBuf pin_small;                   // plan-size read-back, small host outputs
     PinBuf pin_stage, pin_out;          // packed small host batches: inputs, CRCs
@@ -324,7 +323,7 @@ struct Ctx
     {
         if (stream) (void)hipStreamSynchronize(stream);
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
-                          &last_pos, &blk, &longs, &s_ctrl, &s_R, &s_snaps, &s_pval, &srt_cost,
+                          &last_pos, &blk, &longs, &srt_cost,
                           &srt_ctrl, &srt_items})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
@@ -412,35 +411,6 @@ uint32_t apply_zeros(const DeviceState* d, uint32_t s, uint64_t n)
     return s;
 }
 
-// MI_CRC32C_PACKED batches whose span is at least this take the stream path
-// (launch_stream); smaller ones the piece path or the direct kernel.  The
-// stream path is opt-in: on configs[2] it measured 1.06 ms per step against
-// 0.90 ms for the piece path.  The snapshot workspace
-// is 4 KiB per chunk of the span (sparse: only rows holding a record boundary
-// are written), capped here.
-constexpr uint64_t kStreamMin = uint64_t(32) << 20;
-constexpr uint64_t kStreamMaxSpan = uint64_t(32) << 30;
-
-// The stream path (crc32c_kernels.hip, "Sorted batches as one stream") on
-// device arrays: records in address order inside [base + off[0], + span).
-int run_stream(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
-               const uint32_t* inits, size_t count, uint64_t span, uint32_t* out)
-{
-    const uint64_t maxc = stream_max_chunks(span);
-    int st;
-    if ((st = c->s_ctrl.reserve((kStreamCtrlWords + maxc) * 4)) ||
-        (st = c->s_R.reserve(maxc * 4)) || (st = c->s_snaps.reserve(maxc * kChunk)) ||
-        (st = c->s_pval.reserve(uint64_t(count) * 8)) || (st = c->longs.reserve(count * 4)))
-        return st;
-    StreamWorkspace ws{c->s_ctrl.as<uint32_t>(), c->s_ctrl.as<uint32_t>() + kStreamCtrlWords,
-                       c->s_R.as<uint32_t>(),    c->s_snaps.as<uint4>(),
-                       c->s_pval.as<uint32_t>(), c->longs.as<uint32_t>()};
-    HIP_TRY(launch_stream(base, off, len, inits, count, span, ws, out, d->d_tables, d->d_pow2,
-                          d->cus, c->stream));
-    mi_host::note_stream_batch();
-    return MI_CRC32C_OK;
-}
-
 // MI_CRC32C_VARPATH=pieces|sorted: the variable-length path for batches the
 // direct kernel does not take.  Default: the sorted path when the batch's
 // total bytes are known and at least kSortedMinBytes, else the piece path.
@@ -495,19 +465,12 @@ bool plan_scan_forced()
 
 // ---- the variable-length pipeline on device-resident arrays -------------
 // All pointers device pointers; enqueued on c->stream.  `total_bytes` bounds
-// the plan size (0 = unknown -> one read-back).  `span` > 0: the records are
-// in address order inside [base + off[0], + span) (checked by the host for
-// host batches, promised with MI_CRC32C_PACKED and checked on the device for
-// device batches), which lets large batches take the stream path.
+// the plan size (0 = unknown -> one read-back).
 int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
             const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
-            uint64_t max_len = UINT64_MAX,  // longest record if known (host batches)
-            uint64_t span = 0)
+            uint64_t max_len = UINT64_MAX)  // longest record if known (host batches)
 {
     if (count == 0) return MI_CRC32C_OK;
-    if (span >= kStreamMin && span <= kStreamMaxSpan && count < (1ull << 31) &&
-        span <= total_bytes + total_bytes / 4 + (uint64_t(1) << 20))
-        return run_stream(d, c, base, off, len, inits, count, span, out);
     if (count >= (1ull << 31)) return fail(MI_CRC32C_ERANGE, "count >= 2^31 records");
     // items pack addresses in 41 bits (crc32c_kernels.h: Item); user-space and
     // GPU virtual addresses are below 2^47
@@ -603,6 +566,13 @@ extern "C" {
 
 int mi_crc32c_init(int device) { return init_device(device); }
 
+int mi_crc32c_device_pci_bus_id(int device, char* buf, int len)
+{
+    if (!buf || len < 13) return fail(MI_CRC32C_EINVAL, "buffer too small for a PCI bus id");
+    HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
+    return MI_CRC32C_OK;
+}
+
 void* mi_crc32c_stream(void)
 {
     int st = 0;
@@ -651,20 +621,16 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
     if (!c) return st;
     if (flags & MI_CRC32C_DEVICE)
     {
-        const uint64_t span = (flags & MI_CRC32C_PACKED) ? total_bytes : 0;
-        if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out,
-                          UINT64_MAX, span)))
+        if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out)))
             return st;
         return finish(c, flags);
     }
     // Host batch: stage the spanned bytes, rebased offsets, lengths, inits.
     uint64_t lo = UINT64_MAX, hi = 0, total = 0, maxlen = 0;
-    bool ordered = true;  // address order, no overlap: the stream path may take it
     for (size_t i = 0; i < count; ++i)
     {
         if (offsets[i] > UINT64_MAX - lengths[i])
             return fail(MI_CRC32C_EINVAL, "record end overflows 64 bits");
-        if (i + 1 < count && offsets[i + 1] < offsets[i] + lengths[i]) ordered = false;
         if (lengths[i] == 0) continue;
         lo = std::min<uint64_t>(lo, offsets[i]);
         hi = std::max<uint64_t>(hi, offsets[i] + lengths[i]);
@@ -672,11 +638,6 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         maxlen = std::max<uint64_t>(maxlen, lengths[i]);
     }
     if (lo == UINT64_MAX) lo = hi = 0;
-    // MI_CRC32C_PACKED on a host batch: the stream path if the records are in
-    // address order (checked here); it covers [offsets[0], hi)
-    const uint64_t span = (flags & MI_CRC32C_PACKED) && ordered && count && offsets[0] == lo
-                              ? hi - lo
-                              : 0;
     if (hi > lo && !base) return fail(MI_CRC32C_EINVAL, "null base");
     const uint64_t maxlen_arg = (flags & MI_CRC32C_PLANNED) ? UINT64_MAX : maxlen;
     // Small batches (a consus::crc32c call, a durable-log flush): offsets,
@@ -700,7 +661,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
             return st;
         uint8_t* hp = c->pin_stage.as<uint8_t>();
         uint64_t* ho = reinterpret_cast<uint64_t*>(hp);
-        for (size_t i = 0; i < count; ++i) ho[i] = lengths[i] || span ? offsets[i] - lo : 0;
+        for (size_t i = 0; i < count; ++i) ho[i] = lengths[i] ? offsets[i] - lo : 0;
         std::memcpy(hp + count * 8, lengths, count * 4);
         if (inits) std::memcpy(hp + count * 12, inits, count * 4);
         if (!src_pinned && hi > lo)
@@ -734,7 +695,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         if ((st = run_var(d, c, dbase, reinterpret_cast<const uint64_t*>(dp),
                           reinterpret_cast<const uint32_t*>(dp + count * 8),
                           inits ? reinterpret_cast<const uint32_t*>(dp + count * 12) : nullptr,
-                          count, total, c->out.as<uint32_t>(), maxlen_arg, span)))
+                          count, total, c->out.as<uint32_t>(), maxlen_arg)))
             return st;
         HIP_TRY(hipMemcpyAsync(c->pin_out.p, c->out.p, count * 4, hipMemcpyDeviceToHost,
                                c->stream));
@@ -743,7 +704,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         return MI_CRC32C_OK;
     }
     std::vector<uint64_t> reb(count);
-    for (size_t i = 0; i < count; ++i) reb[i] = lengths[i] || span ? offsets[i] - lo : 0;
+    for (size_t i = 0; i < count; ++i) reb[i] = lengths[i] ? offsets[i] - lo : 0;
     if ((st = c->data.reserve(hi - lo + 16)) || (st = c->off.reserve(count * 8)) ||
         (st = c->len.reserve(count * 4)) || (st = c->out.reserve(count * 4)) ||
         (inits && (st = c->inits.reserve(count * 4))))
@@ -757,7 +718,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         HIP_TRY(hipMemcpyAsync(c->inits.p, inits, count * 4, hipMemcpyHostToDevice, c->stream));
     if ((st = run_var(d, c, c->data.p, c->off.as<uint64_t>(), c->len.as<uint32_t>(),
                       inits ? c->inits.as<uint32_t>() : nullptr, count, total,
-                      c->out.as<uint32_t>(), maxlen_arg, span)))
+                      c->out.as<uint32_t>(), maxlen_arg)))
         return st;
     HIP_TRY(hipMemcpyAsync(out, c->out.p, count * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1206,6 +1167,19 @@ int mi_comm_allgather_u32(const uint32_t* dev_send, size_t count, uint32_t* dev_
     const ncclResult_t r = ncclAllGather(dev_send, dev_recv, count, ncclUint32, g_comm, c->stream);
     if (r != ncclSuccess) return fail(MI_CRC32C_ERCCL, ncclGetErrorString(r));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return MI_CRC32C_OK;
+}
+
+int mi_comm_info(int* nranks, int* rank, int* device)
+{
+    if (!g_comm) return fail(MI_CRC32C_EINVAL, "no communicator");
+    ncclResult_t r = ncclSuccess;
+    if (nranks && (r = ncclCommCount(g_comm, nranks)) != ncclSuccess)
+        return fail(MI_CRC32C_ERCCL, ncclGetErrorString(r));
+    if (rank && (r = ncclCommUserRank(g_comm, rank)) != ncclSuccess)
+        return fail(MI_CRC32C_ERCCL, ncclGetErrorString(r));
+    if (device && (r = ncclCommCuDevice(g_comm, device)) != ncclSuccess)
+        return fail(MI_CRC32C_ERCCL, ncclGetErrorString(r));
     return MI_CRC32C_OK;
 }
 

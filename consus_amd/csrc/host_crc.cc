@@ -1,9 +1,10 @@
 // consus_amd/csrc/host_crc.cc -- the engine's CPU path (see host_crc.h).
 //
-// Used only after an engine failure.  Same arithmetic as consus::crc32c
+// Used after an engine failure, and for single host calls below the GPU
+// threshold (size routing, api.cc).  Same arithmetic as consus::crc32c
 // (reflected CRC-32C, poly 0x82F63B78; common/crc32c.cc:122-126): the SSE4.2
 // crc32 instruction over 8-byte words where the host has it, a byte-wise
-// table otherwise.  Deliberately simple: it is a safety net, not a fast path.
+// table otherwise.
 #include "host_crc.h"
 
 #include <atomic>
@@ -66,9 +67,11 @@ bool have_sse42()
 }
 #endif
 
-std::atomic<uint64_t> g_gpu_calls{0}, g_fb_calls{0}, g_fb_bytes{0}, g_sharded{0}, g_stream{0},
-    g_sorted{0};
+std::atomic<uint64_t> g_gpu_calls{0}, g_fb_calls{0}, g_fb_bytes{0}, g_sharded{0}, g_sorted{0},
+    g_routed_calls{0}, g_routed_bytes{0};
 std::atomic<int> g_fb_status{0};
+std::atomic<int> g_multi_ranges{0};
+std::atomic<int> g_multi_devs[MI_CRC32C_MAX_DEVICES];
 
 }  // namespace
 
@@ -107,8 +110,18 @@ void note_fallback(int status, uint64_t bytes)
 
 void note_gpu_call() { g_gpu_calls.fetch_add(1, std::memory_order_relaxed); }
 void note_sharded_call() { g_sharded.fetch_add(1, std::memory_order_relaxed); }
-void note_stream_batch() { g_stream.fetch_add(1, std::memory_order_relaxed); }
 void note_sorted_batch() { g_sorted.fetch_add(1, std::memory_order_relaxed); }
+void note_host_routed(uint64_t bytes)
+{
+    g_routed_calls.fetch_add(1, std::memory_order_relaxed);
+    g_routed_bytes.fetch_add(bytes, std::memory_order_relaxed);
+}
+void note_multi(int ranges, const int* devices)
+{
+    for (int i = 0; i < MI_CRC32C_MAX_DEVICES; ++i)
+        g_multi_devs[i].store(i < ranges ? devices[i] : -1, std::memory_order_relaxed);
+    g_multi_ranges.store(ranges, std::memory_order_relaxed);
+}
 
 }  // namespace mi_host
 
@@ -121,10 +134,14 @@ void mi_crc32c_stats(mi_crc32c_stats_t* out)
     out->fallback_calls = mi_host::g_fb_calls.load();
     out->fallback_bytes = mi_host::g_fb_bytes.load();
     out->sharded_calls = mi_host::g_sharded.load();
-    out->stream_batches = mi_host::g_stream.load();
+    out->host_routed_calls = mi_host::g_routed_calls.load();
+    out->host_routed_bytes = mi_host::g_routed_bytes.load();
     out->sorted_batches = mi_host::g_sorted.load();
     out->last_fallback_status = mi_host::g_fb_status.load();
-    out->reserved = 0;
+    const int ranges = mi_host::g_multi_ranges.load();
+    out->last_multi_ranges = ranges;
+    for (int i = 0; i < MI_CRC32C_MAX_DEVICES; ++i)
+        out->last_multi_devices[i] = i < ranges ? mi_host::g_multi_devs[i].load() : -1;
 }
 
 void mi_crc32c_stats_reset(void)
@@ -133,9 +150,11 @@ void mi_crc32c_stats_reset(void)
     mi_host::g_fb_calls.store(0);
     mi_host::g_fb_bytes.store(0);
     mi_host::g_sharded.store(0);
-    mi_host::g_stream.store(0);
     mi_host::g_sorted.store(0);
+    mi_host::g_routed_calls.store(0);
+    mi_host::g_routed_bytes.store(0);
     mi_host::g_fb_status.store(0);
+    mi_host::g_multi_ranges.store(0);
 }
 
 }  // extern "C"

@@ -1,11 +1,13 @@
 // consus_amd/csrc/host_crc.h -- the engine's own CPU path for CRC-32C.
 //
-// Runs ONLY when the GPU engine cannot (a HIP call failed, no usable gfx950
-// device): it is what makes the drop-in total, as the reference function is
-// (common/crc32c.cc:122-126 cannot fail).  Every use is counted
-// (mi_crc32c_stats); the GPU parity tests assert the count stays 0, so they
-// certify the HIP kernels, never this path.  Product code, independent of the
-// test oracle under oracle/.
+// Runs when the GPU engine cannot (a HIP call failed, no usable gfx950
+// device) -- it is what makes the drop-in total, as the reference function is
+// (common/crc32c.cc:122-126 cannot fail) -- and for single host calls too
+// small to pay a GPU round trip (size routing, mi_crc32c_set_gpu_min).  Every
+// use is counted (mi_crc32c_stats: fallback_calls, host_routed_calls); the GPU
+// parity tests run with the routing threshold at 0 and assert both counts stay
+// 0, so they certify the HIP kernels, never this path.  Product code,
+// independent of the test oracle under oracle/.
 #pragma once
 
 #include <stddef.h>
@@ -28,7 +30,8 @@ void batch_fixed(const void* base, uint64_t stride, uint64_t length, const uint3
 void note_fallback(int status, uint64_t bytes);
 void note_gpu_call();
 void note_sharded_call();
-void note_stream_batch();
 void note_sorted_batch();
+void note_host_routed(uint64_t bytes);
+void note_multi(int ranges, const int* devices);
 
 }  // namespace mi_host

@@ -48,15 +48,6 @@ extern "C" {
                                    planned path (plan -> chunks -> finalize), even
                                    for a batch of short records small enough for
                                    the one-launch direct kernel (tests, tuning) */
-#define MI_CRC32C_PACKED 0x10u  /* batches of >= 32 MiB whose records lie in address order
-                                   without overlap (DEVICE: back to back, offsets[i + 1] ==
-                                   offsets[i] + lengths[i], total_bytes their sum): hash
-                                   them as one stream of aligned 4 KiB chunks instead of
-                                   record pieces.  Checked (host: by the engine before
-                                   staging; device: on the device -- if it does not hold,
-                                   every record is hashed byte-serially, exact but slow).
-                                   Opt-in: measured slower than the default piece path on
-                                   BASELINE configs[2]. */
 #define MI_CRC32C_FALLBACK 0x8u /* host memory only: if the GPU engine fails, complete the
                                    call on the engine's CPU path (counted in
                                    mi_crc32c_stats) instead of returning the failure.
@@ -72,25 +63,46 @@ const char* mi_crc32c_strerror(int status);
 const char* mi_crc32c_last_error(void);
 /* Number of usable (gfx950) devices; does not initialise them. */
 int mi_crc32c_device_count(void);
+/* PCI bus id ("0000:05:00.0") of HIP device `device` into buf (len bytes);
+ * identifies which physical GPU a rank runs on. */
+int mi_crc32c_device_pci_bus_id(int device, char* buf, int len);
 /* The HIP stream (hipStream_t) the calling thread's work is enqueued on. */
 void* mi_crc32c_stream(void);
 int mi_crc32c_stream_sync(void);
 
 /* Counters of the whole process.  The GPU parity tests assert that
- * fallback_calls stays 0: they certify the HIP kernels, not the CPU path. */
+ * fallback_calls and host_routed_calls stay 0: they certify the HIP kernels,
+ * not the CPU path. */
+#define MI_CRC32C_MAX_DEVICES 16
 typedef struct mi_crc32c_stats_t
 {
     uint64_t gpu_calls;           /* compute calls completed by the HIP kernels */
-    uint64_t fallback_calls;      /* calls (or shards) completed by the CPU path */
-    uint64_t fallback_bytes;      /* bytes the CPU path hashed */
+    uint64_t fallback_calls;      /* calls (or shards) completed by the CPU path after an
+                                     engine failure */
+    uint64_t fallback_bytes;      /* bytes the CPU path hashed after engine failures */
     uint64_t sharded_calls;       /* multi-device calls split over more than one range */
-    uint64_t stream_batches;      /* batches hashed by the stream path (records in order) */
+    uint64_t host_routed_calls;   /* single host calls below the GPU threshold answered by the
+                                     CPU path by design (mi_crc32c_set_gpu_min) */
     int32_t last_fallback_status; /* engine status that forced the last fallback (0: none) */
-    int32_t reserved;
+    int32_t last_multi_ranges;    /* ranges of the last multi-device call (0: none yet) */
     uint64_t sorted_batches;      /* variable-length batches hashed by the sorted path */
+    uint64_t host_routed_bytes;   /* bytes of those routed calls */
+    int32_t last_multi_devices[MI_CRC32C_MAX_DEVICES]; /* device ordinal of each range of the
+                                     last multi-device call, in range order (-1: unused) */
 } mi_crc32c_stats_t;
 void mi_crc32c_stats(mi_crc32c_stats_t* out);
 void mi_crc32c_stats_reset(void);
+
+/* Size routing of single host calls: mi_crc32c /
+ * consus::crc32c and mi_crc32c_buffer on HOST memory with n < gpu_min bytes
+ * are answered by the engine's CPU path, without a GPU round trip; larger
+ * ones, every batch and every device buffer go to the GPU.  The default is
+ * the crossover measured on MI355X; env
+ * MI_CRC32C_GPU_MIN (bytes) overrides it at load, this call at run time
+ * (0 = every call on the GPU, as the GPU parity tests run).  Returns the
+ * previous value. */
+uint64_t mi_crc32c_set_gpu_min(uint64_t gpu_min);
+uint64_t mi_crc32c_gpu_min(void);
 
 /* ---- the drop-in -------------------------------------------------------- */
 /* Same signature and semantics as consus::crc32c; never fails (engine failures
@@ -208,6 +220,9 @@ int mi_comm_unique_id(unsigned char id[MI_COMM_ID_BYTES]);
 int mi_comm_init(const unsigned char id[MI_COMM_ID_BYTES], int nranks, int rank);
 /* recv[r * count + i] = send_of_rank_r[i]; device pointers, calling thread's stream */
 int mi_comm_allgather_u32(const uint32_t* dev_send, size_t count, uint32_t* dev_recv);
+/* ranks of the communicator as RCCL counts them (ncclCommCount), this rank
+ * (ncclCommUserRank) and its device (ncclCommCuDevice) */
+int mi_comm_info(int* nranks, int* rank, int* device);
 int mi_comm_destroy(void);
 
 #ifdef __cplusplus

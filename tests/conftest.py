@@ -13,6 +13,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
+# Size routing off (include/consus_crc32c.h, mi_crc32c_set_gpu_min): every
+# call of the suite, and of the tools it starts, goes to the GPU engine, so
+# the GPU tests certify the HIP kernels.  tests/test_routing.py turns it on
+# where it tests it.
+os.environ["MI_CRC32C_GPU_MIN"] = "0"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
@@ -34,15 +40,17 @@ def reference():
 
 @pytest.fixture(autouse=True)
 def _gpu_path_certified(request):
-    """Every GPU test certifies the HIP kernels: the engine's CPU path
-    (mi_crc32c_stats().fallback_calls) must not have run in this process.
-    Tests that exercise the fallback on purpose do it in a subprocess."""
+    """Every GPU test certifies the HIP kernels: the engine's CPU path must not
+    have run in this process, neither after a failure (fallback_calls) nor by
+    size routing (host_routed_calls).  Tests that exercise either on purpose
+    do it in a subprocess."""
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
     import consus_amd
     st = consus_amd.stats()
     assert st["fallback_calls"] == 0, f"CPU-path fallback ran during a GPU test: {st}"
+    assert st["host_routed_calls"] == 0, f"size-routed CPU call during a GPU test: {st}"
 
 
 @pytest.fixture(scope="session")

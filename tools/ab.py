@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 args = sys.argv[1:]
 zipf = "--zipf" in args
-extra = [a for a in args if a.startswith("--") and a != "--zipf"]  # e.g. --packed
+extra = [a for a in args if a.startswith("--") and a != "--zipf"]
 libs = [a for a in args if not a.startswith("--")]
 ablate = os.environ.get("AB_ALLOW_MISMATCH") == "1"  # ablation builds: wrong results expected
 for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):

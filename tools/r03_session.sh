@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-3 GPU session (dev tool): the GPU suite, then the measurement probes
+# named on the command line.  Every GPU step has its own limit; the script
+# stops at the first failure.  Output: gpurun_out/r03/<step>.*
+#   tools/r03_session.sh tests route crossover rehearsal dlog zipf fixed ...
+set -o pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT="$ROOT/gpurun_out/r03"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$ROOT" || exit 9
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" || { echo "FAILED $name rc=$?"; tail -30 "$OUT/$name.out" "$OUT/$name.err"; exit 1; }
+  tail -3 "$OUT/$name.out"
+}
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    route) run route_probe 300 ./tools/route_probe 200 ;;
+    crossover) run crossover 400 python3 -u tools/varpath_crossover.py ;;
+    rehearsal) run bench_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --share-device --steps 5 --warmup 2 --no-cpu ;;
+    dlog) run bench_dlog 300 python bench.py --config dlog --steps 30 ;;
+    zipf) run zipf_probe 300 python3 tools/zipf_probe.py ;;
+    fixed) run fixed_probe 300 python3 tools/perf_probe.py ;;
+    bench) run bench_default 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    ab) shift; AB_ROUNDS=${AB_ROUNDS:-3} run ab 900 python3 -u tools/ab.py --zipf "$@"; break ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "ALL OK"
