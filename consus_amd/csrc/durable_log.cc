@@ -280,8 +280,9 @@ struct durable_log::segment
     struct External
     {
         uint64_t idx;
-        unsigned char* frame;  // header, entry, room for the CRC
-        uint64_t bytes;
+        unsigned char* frame;  // header, entry, room for the CRC; null: malloc failed
+        uint64_t bytes;        // 0 when frame is null
+        uint64_t charged;      // bytes charged to durable_log::m_ext_bytes
     };
     std::mutex ext_mu;
     std::vector<External> ext;
@@ -332,6 +333,8 @@ durable_log::durable_log(const durable_log_options& options)
     , m_frames_flushed(0)
     , m_stop(false)
     , m_fsync_delay_us(0)
+    , m_ext_bytes(0)
+    , m_ext_peak(0)
 {
     for (auto& t : m_flush_ns) t.store(0);
     m_flush = std::thread(&durable_log::flush, this);
@@ -515,9 +518,23 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
     const uint64_t frame = kHeader + entry_sz + kTrailer;
     // Frames of more than half the staging arena are staged outside it
     // (segment::External), so an entry of any size is accepted, as by the
-    // reference (txman/durable_log.cc:187-242).
+    // reference (txman/durable_log.cc:187-242).  Their bytes are charged
+    // before the frame takes a record number and released once the flush
+    // has written it, so they wait for room like a full arena does.
     const bool external = frame > m_capacity / 2;
     const uint64_t arena_bytes = external ? 0 : frame;
+    if (external && !charge_external(frame)) return -1;
+    bool charged = external;  // released by the flush from here on, or below on failure
+    struct Uncharge
+    {
+        durable_log* log;
+        const bool& charged;
+        uint64_t bytes;
+        ~Uncharge()
+        {
+            if (charged) log->release_external(bytes);
+        }
+    } uncharge{this, charged, frame};
     while (true)
     {
         if (const int e = m_error.load())
@@ -557,10 +574,12 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
                 if (external)
                 {
                     // written in record order, just before the arena bytes
-                    // reserved after it (its slot holds that arena offset)
+                    // reserved after it (its slot holds that arena offset);
+                    // the flush releases its charge (a failed malloc's too)
                     std::lock_guard<std::mutex> hold(seg->ext_mu);
-                    seg->ext.push_back(segment::External{idx, p, p ? frame : 0});
+                    seg->ext.push_back(segment::External{idx, p, p ? frame : 0, frame});
                     seg->at_slot(idx) = at | kExternal;
+                    charged = false;
                 }
                 else
                     seg->at_slot(idx) = at;
@@ -645,6 +664,52 @@ int durable_log::error()
     return m_error;
 }
 
+// External frames (more than half an arena) are bounded together, as staged
+// arena bytes are: by both arenas' capacity, but at least 16 MiB (a small
+// arena would otherwise admit one such frame per flush).  An append over the
+// bound waits for the flush to write earlier ones.  A single frame larger
+// than the bound is admitted when none is staged, so an entry of any size is
+// still accepted.
+constexpr uint64_t kExternalMinBudget = uint64_t(16) << 20;
+
+bool durable_log::charge_external(uint64_t bytes)
+{
+    const uint64_t budget = std::max<uint64_t>(2 * uint64_t(m_capacity), kExternalMinBudget);
+    uint64_t cur = m_ext_bytes.load();
+    while (true)
+    {
+        if (cur == 0 || cur + bytes <= budget)
+        {
+            if (!m_ext_bytes.compare_exchange_weak(cur, cur + bytes)) continue;
+            uint64_t peak = m_ext_peak.load();
+            while (cur + bytes > peak && !m_ext_peak.compare_exchange_weak(peak, cur + bytes))
+            {
+            }
+            return true;
+        }
+        std::unique_lock<std::mutex> hold(m_mtx);
+        m_cond.notify_all();  // the flush thread: a staged frame is waiting
+        m_cond.wait(hold, [&] {
+            cur = m_ext_bytes.load();
+            return m_error != 0 || cur == 0 || cur + bytes <= budget;
+        });
+        if (m_error != 0)
+        {
+            errno = m_error;
+            return false;
+        }
+    }
+}
+
+uint64_t durable_log::external_bytes_peak() const { return m_ext_peak.load(); }
+
+void durable_log::release_external(uint64_t bytes)
+{
+    m_ext_bytes.fetch_sub(bytes);
+    std::lock_guard<std::mutex> hold(m_mtx);
+    m_cond.notify_all();
+}
+
 // The batch CRC of n staged frames through the configured engine.  The
 // default engine completes engine failures on the CPU path itself; if an
 // injected test engine fails, the engine's CPU path completes the batch here
@@ -676,7 +741,7 @@ uint32_t durable_log::frame_crc(const unsigned char* frame, uint64_t length)
 // one by one -- patch the CRCs in and write the frames in record order at the
 // end of the file (the sync thread fsyncs it).  Arena frames sit back to
 // back from offset 0; their offsets come from the slots.
-int durable_log::write_segment(segment* seg, uint64_t n, uint64_t used)
+int durable_log::write_segment(segment* seg, uint64_t& n, uint64_t& used)
 {
     auto t = std::chrono::steady_clock::now();
     auto lap = [&](int phase) {
@@ -695,16 +760,38 @@ int durable_log::write_segment(segment* seg, uint64_t n, uint64_t used)
     while (!ext.empty() && ext.back().idx >= n)
     {
         free(ext.back().frame);
+        release_external(ext.back().charged);
         ext.pop_back();
     }
+    // A frame whose staging malloc failed put the log into ENOMEM: nothing
+    // from it on reaches the file (no record-number gap on disk), so the
+    // segment ends at its slot.
+    for (size_t j = 0; j < ext.size(); ++j)
+        if (!ext[j].frame)
+        {
+            n = ext[j].idx;
+            used = seg->at_slot(ext[j].idx) & ~kExternal;
+            for (size_t k = j; k < ext.size(); ++k)
+            {
+                free(ext[k].frame);
+                release_external(ext[k].charged);
+            }
+            ext.resize(j);
+            break;
+        }
     struct Release
     {
+        durable_log* log;
         std::vector<segment::External>& v;
         ~Release()
         {
-            for (segment::External& x : v) free(x.frame);
+            for (segment::External& x : v)
+            {
+                free(x.frame);
+                log->release_external(x.charged);
+            }
         }
-    } release{ext};
+    } release{this, ext};
     if (n)
     {
         m_offs.resize(n);
@@ -994,6 +1081,7 @@ int64_t mi_dlog_replay(mi_dlog* l, void (*f)(void*, const unsigned char*, size_t
 }
 uint64_t mi_dlog_flushes(mi_dlog* l) { return l->log.flushes(); }
 uint64_t mi_dlog_frames_flushed(mi_dlog* l) { return l->log.frames_flushed(); }
+uint64_t mi_dlog_external_peak(mi_dlog* l) { return l->log.external_bytes_peak(); }
 void mi_dlog_flush_seconds(mi_dlog* l, double out[6]) { l->log.flush_seconds(out); }
 void mi_dlog_set_batch_crc_for_testing(mi_dlog* l, mi_dlog_batch_crc fn, void* ctx)
 {

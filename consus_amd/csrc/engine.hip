@@ -307,6 +307,12 @@ struct Ctx
     PinBuf pin_small;                   // plan-size read-back, small host outputs
     PinBuf pin_stage, pin_out;          // packed small host batches: inputs, CRCs
     int ordinal = -1;
+    // set by the last device batch: where its overflow shows when a caller's
+    // size hint was too small (sorted path: ctrl[1] != 0; piece path: the
+    // plan's item total > plan_cap)
+    uint32_t* sorted_ctrl = nullptr;
+    uint32_t* plan_total = nullptr;
+    uint64_t plan_cap = 0;
 
     int open(int dev)
     {
@@ -448,6 +454,7 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
         grid = std::max(1, std::min(8 * grid, std::atoi(e)));
     HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
                           c->stream));
+    c->sorted_ctrl = ws.ctrl;
     mi_host::note_sorted_batch();
     return MI_CRC32C_OK;
 }
@@ -520,6 +527,11 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
         }
         const uint64_t want_grid = (cap + (kBlock / kTeam) - 1) / (kBlock / kTeam);
         const int grid = int(std::min<uint64_t>(uint64_t(d->cus), std::max<uint64_t>(want_grid, 1)));
+        if (total_bytes)
+        {
+            c->plan_total = plan_hdr(c->blk.as<uint32_t>(), nb) + kPlanHdrTotal;
+            c->plan_cap = cap;
+        }
         HIP_TRY(launch_var_chunks(inits, count, ws, d->d_tables, grid, c->stream));
         HIP_TRY(launch_var_finalize(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2,
                                     c->stream));
@@ -621,8 +633,23 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
     if (!c) return st;
     if (flags & MI_CRC32C_DEVICE)
     {
+        c->sorted_ctrl = c->plan_total = nullptr;
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out)))
             return st;
+        if ((flags & MI_CRC32C_ASYNC) || (!c->sorted_ctrl && !c->plan_total))
+            return finish(c, flags);
+        // Synchronous batch sized by the caller's hint: if the hint understated
+        // the sum of lengths, the workspace overflowed and out[] is incomplete
+        // (sorted path: a workgroup found no room for its descriptors; piece
+        // path: the plan exceeded its capacity).  Then hash the batch again
+        // with the plan size read back (total_bytes = 0): exact, slower.
+        uint32_t* flag = c->pin_small.as<uint32_t>() + 1;
+        HIP_TRY(hipMemcpyAsync(flag, c->sorted_ctrl ? c->sorted_ctrl + 1 : c->plan_total, 4,
+                               hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        const bool overflow = c->sorted_ctrl ? *flag != 0 : *flag > c->plan_cap;
+        if (!overflow) return MI_CRC32C_OK;
+        if ((st = run_var(d, c, base, offsets, lengths, inits, count, 0, out))) return st;
         return finish(c, flags);
     }
     // Host batch: stage the spanned bytes, rebased offsets, lengths, inits.

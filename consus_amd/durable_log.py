@@ -29,6 +29,7 @@ _SIGS = {
     "mi_dlog_replay": (C.c_int64, [C.c_void_p, _REPLAY_CB, C.c_void_p]),
     "mi_dlog_flushes": (C.c_uint64, [C.c_void_p]),
     "mi_dlog_frames_flushed": (C.c_uint64, [C.c_void_p]),
+    "mi_dlog_external_peak": (C.c_uint64, [C.c_void_p]),
     "mi_dlog_set_batch_crc_for_testing": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "mi_dlog_set_fsync_delay_for_testing": (None, [C.c_void_p, C.c_uint32]),
     "mi_dlog_flush_seconds": (None, [C.c_void_p, C.POINTER(C.c_double)]),
@@ -99,6 +100,10 @@ class DurableLog:
 
     def frames_flushed(self) -> int:
         return int(_lib().mi_dlog_frames_flushed(self._h))
+
+    def external_peak(self) -> int:
+        """Most bytes of oversized frames staged outside the arenas at once."""
+        return int(_lib().mi_dlog_external_peak(self._h))
 
     def flush_seconds(self) -> list:
         """copy wait, frame walk, batch CRC, CRC patch, pwrite, fsync (s)."""

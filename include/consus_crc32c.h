@@ -121,8 +121,10 @@ int mi_crc32c_buffer(uint32_t init, const void* data, size_t n, uint32_t* out, u
  * Ranges may be unaligned, empty, unordered or overlapping.  total_bytes is
  * the sum of lengths if the caller knows it (0 = unknown: with DEVICE arrays
  * the engine then reads the plan size back once); it must not understate
- * the sum (with DEVICE arrays and an understated hint out[] is left
- * unwritten -- no device read goes out of bounds).
+ * the sum.  With DEVICE arrays and an understated hint no device access goes
+ * out of bounds; a synchronous call detects it and recomputes the batch on
+ * the path that reads its plan size back (exact results, slower); with
+ * MI_CRC32C_ASYNC the contents of out[] are then unspecified.
  * replaces: the per-record call pair crc32c(crc32c(0, header, 16), entry, n)
  *           in durable_log::append, txman/durable_log.cc:215-218 */
 int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,

@@ -37,6 +37,9 @@ int mi_dlog_error(mi_dlog* log);
 int64_t mi_dlog_replay(mi_dlog* log, void (*f)(void*, const unsigned char*, size_t), void* p);
 uint64_t mi_dlog_flushes(mi_dlog* log);
 uint64_t mi_dlog_frames_flushed(mi_dlog* log);
+/* most bytes of oversized frames (more than half a segment, staged outside
+ * the arenas) held at once: bounded by max(segment capacity, largest frame) */
+uint64_t mi_dlog_external_peak(mi_dlog* log);
 /* Seconds the flush thread has spent, summed over flushes, in: [0] waiting
  * for in-flight appends of a sealed segment, [1] walking the frame chain,
  * [2] the batch CRC (GPU), [3] writing the CRCs into the frames, [4] pwrite,

@@ -38,7 +38,10 @@
 #include <thread>
 #include <vector>
 
-namespace consus {
+// consus
+#include "namespace.h"
+
+BEGIN_CONSUS_NAMESPACE
 
 // CRC engine for a batch of frames (default: the GPU, mi_crc32c_batch_multi).
 typedef int (*durable_log_batch_crc)(void* ctx, const void* base, const uint64_t* offsets,
@@ -56,7 +59,11 @@ struct durable_log_options
                                    // devices; 0 = the engine's measured default (4 MiB)
 };
 
-class durable_log
+// As in the reference, the class sits in Consus's hidden-visibility namespace
+// (namespace.h:4-5).  The reference compiles durable_log.cc into the txman
+// executable; here libconsus_crc32c.so carries it (with the mi_dlog_* C ABI),
+// so the class alone is given default visibility to be linkable from it.
+class __attribute__((visibility("default"))) durable_log
 {
     public:
         durable_log();
@@ -87,6 +94,9 @@ class durable_log
         void flush_seconds(double out[6]) const;
         // Test hook: every fsync also sleeps this long (a slow disk on tmpfs).
         void set_fsync_delay_for_testing(uint32_t microseconds);
+        // Most bytes of oversized frames (staged outside the arenas) held at
+        // once: at most max(segment capacity, the largest such frame).
+        uint64_t external_bytes_peak() const;
 
     private:
         struct segment;
@@ -100,7 +110,9 @@ class durable_log
         void sync();
         int64_t append_slow(segment* seg);
         void switch_to_next(segment* seg, uint64_t n);
-        int write_segment(segment* seg, uint64_t nframes, uint64_t used);
+        int write_segment(segment* seg, uint64_t& nframes, uint64_t& used);
+        bool charge_external(uint64_t bytes);
+        void release_external(uint64_t bytes);
         int batch_crc(const unsigned char* base, const uint64_t* offs, const uint32_t* lens,
                       size_t n, uint64_t total, uint32_t* out);
         uint32_t frame_crc(const unsigned char* frame, uint64_t length);
@@ -135,12 +147,16 @@ class durable_log
         std::vector<synced> m_pending;  // under m_mtx: at most one written, unsynced segment
         bool m_stop;                    // under m_mtx: the destructor ends the sync thread
         std::atomic<uint32_t> m_fsync_delay_us;
+        // bytes of frames staged outside the arenas (entries of more than
+        // half a segment), both segments together; bounded like the arenas
+        std::atomic<uint64_t> m_ext_bytes;
+        std::atomic<uint64_t> m_ext_peak;
 
     private:
         durable_log(const durable_log&);
         durable_log& operator = (const durable_log&);
 };
 
-}  // namespace consus
+END_CONSUS_NAMESPACE
 
 #endif // consus_txman_log_h_

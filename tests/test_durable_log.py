@@ -189,6 +189,39 @@ def test_oversized_entries_concurrent(make_log, tmp_path):
     assert log.replay() == [got[r] for r in range(1, 241)]
 
 
+def test_oversized_entries_memory_is_bounded(make_log, tmp_path):
+    """frames of more than half a segment are staged outside the
+    arenas; a producer faster than the disk must not grow them without bound.
+    With every fsync slowed to 2 ms, 4 threads append 9 and 20 MiB entries
+    into a log of 16 MiB segments: the bytes staged outside the arenas never
+    exceed max(2 x 16 MiB, the largest frame), and every record replays."""
+    cap = 16 << 20
+    log = make_log(capacity=cap)
+    log.set_fsync_delay_for_testing(2000)
+    assert log.open(str(tmp_path / "d"))
+    got = {}
+
+    def worker(t):
+        for i in range(6):
+            n = (9 << 20) if (i + t) % 3 else (20 << 20)
+            e = bytes([t, i]) + bytes(n - 2)
+            r = log.append(e)
+            assert r > 0
+            got[r] = (t, i, n)
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    wait_durable(log, 24)
+    peak = log.external_peak()
+    log.close()
+    assert 0 < peak <= max(2 * cap, (20 << 20) + 20), peak
+    assert sorted(got) == list(range(1, 25))
+    back = log.replay()
+    assert [(e[0], e[1], len(e)) for e in back] == [got[r] for r in range(1, 25)]
+
+
 def test_close_with_concurrent_appenders(make_log, tmp_path):
     """close() waits only for the records reserved before it was called, so
     appenders that keep going cannot hold it up (the reference's close,

@@ -4,6 +4,7 @@ mi_crc32c_last_error(), nothing is launched, and the engine keeps working
 for the next valid call.  The reference function has no error channel
 (common/crc32c.h:40-41); these are the status codes of the batch ABI."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -108,11 +109,15 @@ def test_device_helper_errors(L, engine):
     recv.free()
 
 
-def test_understated_size_hint_leaves_out_unwritten(engine, oracle):
-    """A total_bytes hint below the true sum sizes the plan workspace too
-    small: every plan, chunk and finalize kernel sees the overflow and
-    writes nothing (no out-of-bounds access); the next call with a true
-    hint, or none, is exact."""
+def test_understated_size_hint_is_recovered(engine, oracle):
+    """A total_bytes hint below the true sum sizes the workspace too small:
+    no kernel accesses out of bounds, and a synchronous call sees the
+    overflow and recomputes the batch with the plan size read back, so its
+    results are exact -- on the piece path and on the sorted path (ADVICE
+    r2: the sorted path used to return OK with partial results).  The calls
+    run in fresh threads: their own contexts, so their workspaces are sized by
+    the understated hint alone (grow-only buffers of earlier calls would fit)."""
+    import threading
     rng = np.random.default_rng(3)
     count = 64
     lengths = np.full(count, 1 << 20, dtype=np.uint32)   # 256+ pieces per record
@@ -125,24 +130,27 @@ def test_understated_size_hint_leaves_out_unwritten(engine, oracle):
                            engine.DeviceBuffer(count * 4))
     d_off.upload(offsets)
     d_len.upload(lengths)
-    sentinel = np.full(count, 0xABABABAB, dtype=np.uint32)
-    d_out.upload(sentinel)
-    # in a fresh thread: its own context, so its workspaces are sized by
-    # this call's hint alone (grow-only buffers of earlier calls would fit)
-    import threading
-    errors = []
-
-    def understated():
-        try:
-            engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=4096)
-        except Exception as e:  # noqa: BLE001
-            errors.append(e)
-    t = threading.Thread(target=understated)
-    t.start()
-    t.join()
-    assert not errors, errors[0]
-    assert np.array_equal(d_out.download(np.uint32, count), sentinel)
     want = oracle.batch(buf, offsets, lengths)
+    # a 4 KiB hint on the piece path; a 4 MiB hint (room for 129 descriptors)
+    # on the sorted path, whose split records need 64 + 960 of them
+    for hint, path in ((4096, None), (4 << 20, "sorted")):
+        d_out.upload(np.full(count, 0xABABABAB, dtype=np.uint32))
+        errors = []
+
+        def understated():
+            try:
+                if path:
+                    os.environ["MI_CRC32C_VARPATH"] = path
+                engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=hint)
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+            finally:
+                os.environ.pop("MI_CRC32C_VARPATH", None)
+        t = threading.Thread(target=understated)
+        t.start()
+        t.join()
+        assert not errors, errors[0]
+        assert np.array_equal(d_out.download(np.uint32, count), want), (hint, path)
     for hint in (int(lengths.sum()), 0):
         engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=hint)
         assert np.array_equal(d_out.download(np.uint32, count), want)

@@ -15,7 +15,8 @@ run() {  # name limit cmd...
   timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" || { echo "FAILED $name rc=$?"; tail -30 "$OUT/$name.out" "$OUT/$name.err"; exit 1; }
   tail -3 "$OUT/$name.out"
 }
-for step in "$@"; do
+while [ $# -gt 0 ]; do
+  step=$1; shift
   case $step in
     tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -27,7 +28,17 @@ for step in "$@"; do
     zipf) run zipf_probe 300 python3 tools/zipf_probe.py ;;
     fixed) run fixed_probe 300 python3 tools/perf_probe.py ;;
     bench) run bench_default 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
-    ab) shift; AB_ROUNDS=${AB_ROUNDS:-3} run ab 900 python3 -u tools/ab.py --zipf "$@"; break ;;
+    shortab) for rnd in 1 2 3; do for v in 0 256 1024 4096; do
+               echo -n "round $rnd short=$v "; MI_CRC32C_SORT_SHORT=$v timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done; done | tee "$OUT/shortab.out" ;;
+    shortiso) for rnd in 1 2; do for cfg in "0 -" "1024 -" "256 -" "1024 keep" "0 keep" "0 drop" "1024 drop"; do
+               set -- $cfg; v=$1; m=$2; envs="MI_CRC32C_SORT_SHORT=$v"
+               [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
+               echo -n "round $rnd short=$v class=$m "; env $envs timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done; done | tee "$OUT/shortiso.out"; set -- ;;
+    sorted) run pytest_sorted 600 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread ;;
+    ab) AB_ROUNDS=${AB_ROUNDS:-3} run ab 900 python3 -u tools/ab.py --zipf "$@"; break ;;
+    abfixed) AB_ROUNDS=${AB_ROUNDS:-3} run abfixed 900 python3 -u tools/ab.py "$@"; break ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
