@@ -377,33 +377,68 @@ def run_dlog(args) -> dict:
     watermark to cover them, then the log is replayed (GPU-verified scan of
     both segment files) and every record checked byte-exact.  Segment files
     on tmpfs (/dev/shm): fsync is free there, so this is the front-end and
-    GPU-batch rate, not a disk's."""
+    batch-CRC rate, not a disk's.  Same run, interleaved: the same front-end
+    with the reference common/crc32c.cc (oracle/_ref) as the flush thread's
+    checksum (txman/durable_log.cc:187-242 calls it per record) -- the CPU
+    baseline of this line."""
     exe = os.path.join(REPO, "tools", "dlog_bench")
     d = tempfile.mkdtemp(prefix="dlog_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
     threads, per = 8, 400_000
-    runs = []
+    from oracle.oracle import REF_SO, reference_available
+    engines = [("gpu", {})]
+    if reference_available() and not args.no_cpu:
+        engines.append(("reference-cpu", {"REF_CRC_SO": REF_SO}))
+    runs = {name: [] for name, _ in engines}
     try:
         for _ in range(max(1, args.steps // 10)):
-            r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(per), "42", "1024"],
-                               capture_output=True, text=True, timeout=300)
-            if r.returncode != 0:
-                raise RuntimeError(f"dlog_bench failed: {r.stdout[-500:]} {r.stderr[-500:]}")
-            runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
-            shutil.rmtree(os.path.join(d, "log"), ignore_errors=True)
+            for name, extra in engines:
+                env = dict(os.environ)
+                env.update(extra)
+                r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(per), "42", "1024"],
+                                   capture_output=True, text=True, timeout=300, env=env)
+                if r.returncode != 0:
+                    raise RuntimeError(f"dlog_bench ({name}) failed: {r.stdout[-500:]} {r.stderr[-500:]}")
+                runs[name].append(json.loads(r.stdout.strip().splitlines()[-1]))
+                shutil.rmtree(os.path.join(d, "log"), ignore_errors=True)
     finally:
         shutil.rmtree(d, ignore_errors=True)
-    best = sorted(runs, key=lambda x: x["appends_per_s"])[(len(runs) - 1) // 2]  # (lower) median
+
+    def median(rs):
+        return sorted(rs, key=lambda x: x["appends_per_s"])[(len(rs) - 1) // 2]  # (lower) median
+
+    def per_flush(x):
+        f = max(x["flushes"], 1)
+        return {"flushes": x["flushes"], "frame_bytes_per_flush": round(x["frame_bytes"] / f),
+                "us_per_flush": {k: round(v / f * 1e6, 2) for k, v in x["flush_s"].items()}}
+    best = median(runs["gpu"])
+    pf = per_flush(best)
+    # the per-flush bound of the GPU batch: one launch-and-sync round trip
+    # (~13 us measured for an empty zero-copy launch, DESIGN.md section 4.4)
+    # plus the flush's bytes at the host link's ~55 GB/s
+    bound = 13.0 + pf["frame_bytes_per_flush"] / 55e3
+    pf["batch_crc_bound_us"] = round(bound, 2)
+    pf["batch_crc_vs_bound"] = round(pf["us_per_flush"]["batch_crc"] / bound, 3)
+    cpu = None
+    if "reference-cpu" in runs:
+        rb = median(runs["reference-cpu"])
+        cpu = {"value": round(rb["appends_per_s"], 1), "unit": "appends/s", "cores": 1,
+               "kind": "reference",
+               "sample": "the same front-end, appenders and entries, with the flush thread's "
+                         "batch checksum done by the reference common/crc32c.cc (oracle/_ref, "
+                         "compiled unmodified; crc32q dispatch) frame by frame on that thread",
+               "per_flush": per_flush(rb), "runs": runs["reference-cpu"]}
     return {"metric": "durable-log appends/s, 8 appending threads, GPU batch CRC per flushed "
                       "segment (txman/durable_log.cc append contract)",
             "value": round(best["appends_per_s"], 1), "unit": "appends/s", "n_gpus": 1,
-            "steps": len(runs), "warmup": 0, "ms_per_step": round(best["durable_s"] * 1e3, 3),
+            "steps": len(runs["gpu"]), "warmup": 0, "ms_per_step": round(best["durable_s"] * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: entry lengths uniform 42-1024 B, splitmix64 bytes",
             "config": {"workload": f"{threads} threads x {per} appends, then wait for the "
-                                   f"watermark; segment files on tmpfs", "runs": runs},
-            "roofline": None, "cpu_baseline": None,
+                                   f"watermark; segment files on tmpfs", "runs": runs["gpu"]},
+            "flush": pf,
+            "roofline": None, "cpu_baseline": cpu,
             "digest_verified": all(x["replayed"] == x["appends"] and x["replay_bad"] == 0
-                                   for x in runs)}
+                                   for rs in runs.values() for x in rs)}
 
 
 def run_secondary(args, E, traffic=(None, "skipped")) -> dict:

@@ -119,7 +119,8 @@ class Stats(C.Structure):
                 ("last_multi_ranges", C.c_int32),
                 ("sorted_batches", C.c_uint64),
                 ("host_routed_bytes", C.c_uint64),
-                ("last_multi_devices", C.c_int32 * MAX_DEVICES)]
+                ("last_multi_devices", C.c_int32 * MAX_DEVICES),
+                ("zero_copy_batches", C.c_uint64)]
 
 _lib = None
 

@@ -9,8 +9,10 @@
 // offset) with one fetch-and-add on the active segment instead of two
 // m_mtx sections (:195-213, :232-239) -- under 8 appending threads the lock
 // hand-offs cut throughput ~9x -- and stages the frame in pinned memory; the
-// flush thread checksums each sealed segment in one GPU batch, then writes it
-// with one pwrite and fsyncs it.
+// flush thread checksums each sealed segment in one GPU batch (read in place
+// from the mapped staging arena), a writer thread pwrites it while the next
+// segment is checksummed (the arena rotates through a third, spare one), and
+// a sync thread fsyncs it and publishes the watermark.
 
 #include "../../include/txman/durable_log.h"
 
@@ -289,6 +291,34 @@ struct durable_log::segment
     bool pinned = false;  // arena from mi_host_malloc_pinned (else malloc)
 };
 
+// A checksummed segment handed from the flush thread to the writer: its
+// arena (the segment itself has moved on to the spare arena) with the frames
+// at [0, used), the external frames and the arena offsets they precede, and
+// where they go in which file.  Frees what it still holds.
+struct durable_log::write_job
+{
+    durable_log* log = nullptr;
+    unsigned char* arena = nullptr;
+    bool arena_pinned = false;
+    uint64_t used = 0;
+    std::vector<segment::External> ext;
+    std::vector<uint64_t> ext_at;
+    int fd = -1;
+    uint64_t file_off = 0;
+    uint64_t upto = 0;    // watermark once written and synced
+    uint64_t frames = 0;
+    void release_ext()
+    {
+        for (segment::External& x : ext)
+        {
+            free(x.frame);
+            log->release_external(x.charged);
+        }
+        ext.clear();
+    }
+    ~write_job() { release_ext(); }
+};
+
 static unsigned done_shard()
 {
     static std::atomic<unsigned> next{0};
@@ -331,6 +361,9 @@ durable_log::durable_log(const durable_log_options& options)
     , m_pinned(true)
     , m_flushes(0)
     , m_frames_flushed(0)
+    , m_spare(nullptr)
+    , m_spare_pinned(false)
+    , m_stop_writer(false)
     , m_stop(false)
     , m_fsync_delay_us(0)
     , m_ext_bytes(0)
@@ -338,6 +371,7 @@ durable_log::durable_log(const durable_log_options& options)
 {
     for (auto& t : m_flush_ns) t.store(0);
     m_flush = std::thread(&durable_log::flush, this);
+    m_writer = std::thread(&durable_log::writer, this);
     m_sync = std::thread(&durable_log::sync, this);
 }
 
@@ -347,10 +381,22 @@ durable_log::~durable_log() throw()
     if (m_flush.joinable()) m_flush.join();
     {
         std::lock_guard<std::mutex> hold(m_mtx);
+        m_stop_writer = true;  // the writer drains its job first
+        m_cond.notify_all();
+    }
+    if (m_writer.joinable()) m_writer.join();
+    {
+        std::lock_guard<std::mutex> hold(m_mtx);
         m_stop = true;
         m_cond.notify_all();
     }
     if (m_sync.joinable()) m_sync.join();
+    for (write_job* j : m_jobs)
+    {
+        if (j->arena) j->arena_pinned ? (void)mi_host_free_pinned(j->arena) : free(j->arena);
+        delete j;
+    }
+    if (m_spare) m_spare_pinned ? (void)mi_host_free_pinned(m_spare) : free(m_spare);
     for (segment* s : {m_segment_a, m_segment_b})
     {
         if (!s) continue;
@@ -440,6 +486,16 @@ bool durable_log::open(const std::string& dir)
     }
     segment* segs[2] = {new segment, new segment};
     const int fds[2] = {file_a, file_b};
+    // the third arena: a checksummed segment's bytes go to the writer in
+    // their arena while the segment continues in this one
+    {
+        void* p = nullptr;
+        if (m_pinned && mi_host_malloc_pinned(&p, m_capacity) == MI_CRC32C_OK)
+            m_spare_pinned = true;
+        else
+            p = malloc(m_capacity);
+        m_spare = static_cast<unsigned char*>(p);
+    }
     // at most one frame per 20 staged bytes, and headroom below the
     // reservation word's frame field (no carry into the sealed bit)
     const uint64_t frames = std::min<uint64_t>(m_capacity / (kHeader + kTrailer) + 1,
@@ -462,8 +518,10 @@ bool durable_log::open(const std::string& dir)
         segs[i]->at = new (std::nothrow) uint64_t[segs[i]->slots];
         ok = ok && p && segs[i]->at;
     }
-    if (!ok)
+    if (!ok || !m_spare)
     {
+        if (m_spare) m_spare_pinned ? (void)mi_host_free_pinned(m_spare) : free(m_spare);
+        m_spare = nullptr;
         m_error = ENOMEM;
         for (segment* s : segs)
         {
@@ -738,10 +796,10 @@ uint32_t durable_log::frame_crc(const unsigned char* frame, uint64_t length)
 }
 
 // Checksum the segment's n frames -- the arena's in one batch, external ones
-// one by one -- patch the CRCs in and write the frames in record order at the
-// end of the file (the sync thread fsyncs it).  Arena frames sit back to
-// back from offset 0; their offsets come from the slots.
-int durable_log::write_segment(segment* seg, uint64_t& n, uint64_t& used)
+// one by one -- and patch the CRCs in; fill `job` with what the writer needs
+// to write them in record order at the end of the file.  Arena frames sit
+// back to back from offset 0; their offsets come from the slots.
+int durable_log::prepare_segment(segment* seg, uint64_t& n, uint64_t& used, write_job* job)
 {
     auto t = std::chrono::steady_clock::now();
     auto lap = [&](int phase) {
@@ -749,11 +807,12 @@ int durable_log::write_segment(segment* seg, uint64_t& n, uint64_t& used)
         m_flush_ns[phase] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(u - t).count());
         t = u;
     };
-    std::vector<segment::External> ext;
+    job->log = this;
     {
         std::lock_guard<std::mutex> hold(seg->ext_mu);
-        ext.swap(seg->ext);
+        job->ext.swap(seg->ext);
     }
+    std::vector<segment::External>& ext = job->ext;
     std::sort(ext.begin(), ext.end(),
               [](const segment::External& x, const segment::External& y) { return x.idx < y.idx; });
     // frames past the cut were never handed out (their appenders retried)
@@ -779,19 +838,8 @@ int durable_log::write_segment(segment* seg, uint64_t& n, uint64_t& used)
             ext.resize(j);
             break;
         }
-    struct Release
-    {
-        durable_log* log;
-        std::vector<segment::External>& v;
-        ~Release()
-        {
-            for (segment::External& x : v)
-            {
-                free(x.frame);
-                log->release_external(x.charged);
-            }
-        }
-    } release{this, ext};
+    job->ext_at.resize(ext.size());
+    for (size_t j = 0; j < ext.size(); ++j) job->ext_at[j] = seg->at_slot(ext[j].idx) & ~kExternal;
     if (n)
     {
         m_offs.resize(n);
@@ -813,29 +861,85 @@ int durable_log::write_segment(segment* seg, uint64_t& n, uint64_t& used)
         lap(1);
         if (k) batch_crc(seg->arena, m_offs.data(), m_lens.data(), size_t(k), total, m_crcs.data());
         for (segment::External& x : ext)
-            if (x.frame)
-                pack32be(frame_crc(x.frame, x.bytes - kTrailer), x.frame + x.bytes - kTrailer);
+            pack32be(frame_crc(x.frame, x.bytes - kTrailer), x.frame + x.bytes - kTrailer);
         lap(2);
         // crc32c(crc32c(0, header, 16), entry) == crc32c(0, header || entry),
         // stored big-endian after the entry (txman/durable_log.cc:215-224)
         for (uint64_t i = 0; i < k; ++i) pack32be(m_crcs[i], seg->arena + m_offs[i] + m_lens[i]);
         lap(3);
     }
-    uint64_t at = 0, file = seg->file_size;
-    for (const segment::External& x : ext)
+    uint64_t bytes = used;
+    for (const segment::External& x : ext) bytes += x.bytes;
+    job->used = used;
+    job->fd = seg->fd;
+    job->file_off = seg->file_size;
+    job->upto = seg->base + n;
+    job->frames = n;
+    seg->file_size += bytes;
+    return 0;
+}
+
+// The writer's half: the job's frames in record order at its file offset.
+int durable_log::write_out(write_job* job)
+{
+    const auto t = std::chrono::steady_clock::now();
+    uint64_t at = 0, file = job->file_off;
+    for (size_t j = 0; j < job->ext.size(); ++j)
     {
-        const uint64_t upto = seg->at_slot(x.idx) & ~kExternal;
-        if (upto > at && !pwrite_all(seg->fd, seg->arena + at, upto - at, off_t(file))) return errno;
+        const segment::External& x = job->ext[j];
+        const uint64_t upto = job->ext_at[j];
+        if (upto > at && !pwrite_all(job->fd, job->arena + at, upto - at, off_t(file))) return errno;
         file += upto - at;
         at = upto;
-        if (x.bytes && !pwrite_all(seg->fd, x.frame, x.bytes, off_t(file))) return errno;
+        if (x.bytes && !pwrite_all(job->fd, x.frame, x.bytes, off_t(file))) return errno;
         file += x.bytes;
     }
-    if (used > at && !pwrite_all(seg->fd, seg->arena + at, used - at, off_t(file))) return errno;
-    file += used - at;
-    lap(4);
-    seg->file_size = file;
+    if (job->used > at &&
+        !pwrite_all(job->fd, job->arena + at, job->used - at, off_t(file)))
+        return errno;
+    job->release_ext();
+    m_flush_ns[4] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                  std::chrono::steady_clock::now() - t)
+                                  .count());
     return 0;
+}
+
+// The writer thread: write each checksummed segment, give its arena back as
+// the spare, and hand the fsync to the sync thread (at most one written
+// segment waits for it, so appends stay throttled by the disk).  It runs
+// beside the flush thread, which meanwhile checksums the next segment.
+void durable_log::writer()
+{
+    sigset_t ss;
+    if (sigfillset(&ss) == 0) pthread_sigmask(SIG_BLOCK, &ss, nullptr);
+    std::unique_lock<std::mutex> hold(m_mtx);
+    while (true)
+    {
+        m_cond.wait(hold, [&] { return m_stop_writer || !m_jobs.empty(); });
+        if (m_jobs.empty()) return;  // m_stop_writer, nothing left to write
+        write_job* job = m_jobs.front();
+        m_jobs.erase(m_jobs.begin());
+        hold.unlock();
+        const int e = m_error.load() > 0 ? 0 : write_out(job);
+        hold.lock();
+        m_spare = job->arena;  // free again: the next sealed segment may take it
+        m_spare_pinned = job->arena_pinned;
+        job->arena = nullptr;
+        if (e && (m_error == 0 || m_error == -1)) m_error = e;
+        m_cond.notify_all();
+        if (m_error == 0 || m_error == -1)
+        {
+            m_cond.wait(hold, [&] { return (m_error != 0 && m_error != -1) || m_pending.empty(); });
+            if (m_error == 0 || m_error == -1)
+            {
+                m_pending.push_back(synced{job->fd, job->upto, job->frames});
+                m_cond.notify_all();
+            }
+        }
+        hold.unlock();
+        delete job;  // frees external frames a failed write left behind
+        hold.lock();
+    }
 }
 
 // The sync thread: fsync each written segment in turn and publish its
@@ -962,21 +1066,34 @@ void durable_log::flush()
             std::lock_guard<std::mutex> hold(m_mtx);
             switch_to_next(seg, n);
         }
-        const int e = write_segment(seg, n, used);
+        auto* job = new write_job;
+        const int e = prepare_segment(seg, n, used, job);
         {
             std::unique_lock<std::mutex> hold(m_mtx);
             if (e)
             {
                 m_error = e;
                 m_cond.notify_all();
+                hold.unlock();
+                delete job;
                 return;
             }
-            // hand the fsync to the sync thread; at most one written segment
-            // waits for it, so appends stay throttled by the disk as with
-            // one segment being fsynced while appends go to the other
-            m_cond.wait(hold, [&] { return m_error != 0 || m_pending.empty(); });
-            if (m_error != 0) return;
-            m_pending.push_back(synced{seg->fd, seg->base + n, n});
+            // hand the bytes to the writer in their arena; the segment takes
+            // the spare one (back from the writer's previous job) before it
+            // can be active again
+            m_cond.wait(hold, [&] { return m_error != 0 || m_spare != nullptr; });
+            if (m_error != 0)
+            {
+                hold.unlock();
+                delete job;
+                return;
+            }
+            job->arena = seg->arena;
+            job->arena_pinned = seg->pinned;
+            seg->arena = m_spare;
+            seg->pinned = m_spare_pinned;
+            m_spare = nullptr;
+            m_jobs.push_back(job);
             m_cond.notify_all();
         }
     }

@@ -399,6 +399,21 @@ Ctx* thread_ctx_on(int dev, DeviceState** dout, int* status)
 
 Ctx* thread_ctx(int* status) { return thread_ctx_on(-1, nullptr, status); }
 
+// The device's address of host bytes in mapped pinned memory (hipHostMalloc
+// with hipHostMallocMapped, e.g. a durable-log staging arena), else null.
+const uint8_t* mapped_device_ptr(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    return static_cast<const uint8_t*>(a.devicePointer) +
+           (static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(a.hostPointer));
+}
+
 bool is_pinned(const void* p)
 {
     hipPointerAttribute_t a;
@@ -457,6 +472,14 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     c->sorted_ctrl = ws.ctrl;
     mi_host::note_sorted_batch();
     return MI_CRC32C_OK;
+}
+
+// MI_CRC32C_ZERO_COPY=0: host batches in mapped pinned memory are staged by
+// copy commands instead of read in place (A/B and tests; read per batch)
+bool zero_copy_disabled()
+{
+    const char* e = std::getenv("MI_CRC32C_ZERO_COPY");
+    return e && !std::strcmp(e, "0");
 }
 
 // MI_CRC32C_PLAN_SCAN=1: plans always take the separate scan pass (which
@@ -667,6 +690,41 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
     if (lo == UINT64_MAX) lo = hi = 0;
     if (hi > lo && !base) return fail(MI_CRC32C_EINVAL, "null base");
     const uint64_t maxlen_arg = (flags & MI_CRC32C_PLANNED) ? UINT64_MAX : maxlen;
+    // Bytes already in mapped pinned memory (a durable-log flush: the staging
+    // arena is mapped) and a batch the one-launch direct kernel takes: the
+    // kernel reads the records where they lie, over PCIe (zero-copy), and
+    // the offsets, lengths and CRCs through mapped pinned staging too -- one
+    // launch and one sync, no copy command.  (Two copy commands around the
+    // kernel cost ~40 us more per 550 KB flush: DESIGN.md section 7.)
+    if (hi > lo && maxlen_arg <= kDirectMaxRecord && total <= kDirectMaxBytes &&
+        count <= kDirectMaxCount && !zero_copy_disabled())
+    {
+        if (const uint8_t* zsrc = mapped_device_ptr(static_cast<const uint8_t*>(base) + lo))
+        {
+            const uint64_t meta_bytes = uint64_t(count) * (inits ? 16 : 12);
+            if ((st = c->pin_stage.reserve(meta_bytes + 16)) || (st = c->pin_out.reserve(count * 4)))
+                return st;
+            if (c->pin_stage.dev && c->pin_out.dev)
+            {
+                uint8_t* hp = c->pin_stage.as<uint8_t>();
+                uint64_t* ho = reinterpret_cast<uint64_t*>(hp);
+                for (size_t i = 0; i < count; ++i) ho[i] = lengths[i] ? offsets[i] - lo : 0;
+                std::memcpy(hp + count * 8, lengths, count * 4);
+                if (inits) std::memcpy(hp + count * 12, inits, count * 4);
+                const uint8_t* sp = static_cast<const uint8_t*>(c->pin_stage.dev);
+                HIP_TRY(launch_direct(zsrc, reinterpret_cast<const uint64_t*>(sp),
+                                      reinterpret_cast<const uint32_t*>(sp + count * 8),
+                                      inits ? reinterpret_cast<const uint32_t*>(sp + count * 12)
+                                            : nullptr,
+                                      count, static_cast<uint32_t*>(c->pin_out.dev), d->d_tables,
+                                      d->d_pow2, d->cus, c->stream));
+                HIP_TRY(hipStreamSynchronize(c->stream));
+                std::memcpy(out, c->pin_out.p, count * 4);
+                mi_host::note_zero_copy_batch();
+                return MI_CRC32C_OK;
+            }
+        }
+    }
     // Small batches (a consus::crc32c call, a durable-log flush): offsets,
     // lengths, inits -- and the bytes, unless they already sit in pinned
     // memory -- packed into one pinned staging buffer and moved with ONE
@@ -1087,7 +1145,10 @@ int mi_host_malloc_pinned(void** p, size_t bytes)
     int st = 0;
     if (!p) return fail(MI_CRC32C_EINVAL, "null out pointer");
     if (!dev_or_init(&st)) return st;
-    if (hipHostMalloc(p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess)
+    // mapped (and portable: every device's address space), so batches over
+    // these bytes can be read in place by the kernels (zero-copy)
+    if (hipHostMalloc(p, std::max<size_t>(bytes, 1), hipHostMallocMapped | hipHostMallocPortable) !=
+        hipSuccess)
         return fail(MI_CRC32C_ENOMEM, "hipHostMalloc(" + std::to_string(bytes) + ") failed");
     return MI_CRC32C_OK;
 }

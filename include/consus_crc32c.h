@@ -89,6 +89,8 @@ typedef struct mi_crc32c_stats_t
     uint64_t host_routed_bytes;   /* bytes of those routed calls */
     int32_t last_multi_devices[MI_CRC32C_MAX_DEVICES]; /* device ordinal of each range of the
                                      last multi-device call, in range order (-1: unused) */
+    uint64_t zero_copy_batches;   /* host batches the kernels read in place from mapped
+                                     pinned memory (mi_host_malloc_pinned) */
 } mi_crc32c_stats_t;
 void mi_crc32c_stats(mi_crc32c_stats_t* out);
 void mi_crc32c_stats_reset(void);

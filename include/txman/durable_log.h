@@ -100,6 +100,7 @@ class __attribute__((visibility("default"))) durable_log
 
     private:
         struct segment;
+        struct write_job;                   // a checksummed segment's bytes for the writer
         struct synced                       // a written segment awaiting fsync
         {
             int fd;
@@ -107,10 +108,12 @@ class __attribute__((visibility("default"))) durable_log
             uint64_t frames;
         };
         void flush();
+        void writer();
         void sync();
         int64_t append_slow(segment* seg);
         void switch_to_next(segment* seg, uint64_t n);
-        int write_segment(segment* seg, uint64_t& nframes, uint64_t& used);
+        int prepare_segment(segment* seg, uint64_t& nframes, uint64_t& used, write_job* job);
+        int write_out(write_job* job);
         bool charge_external(uint64_t bytes);
         void release_external(uint64_t bytes);
         int batch_crc(const unsigned char* base, const uint64_t* offs, const uint32_t* lens,
@@ -124,6 +127,7 @@ class __attribute__((visibility("default"))) durable_log
         std::mutex m_mtx;               // flush hand-offs, waiters; never on the append fast path
         std::condition_variable m_cond;
         std::thread m_flush;
+        std::thread m_writer;           // pwrites checksummed segments (beside the next CRC)
         std::thread m_sync;             // fsyncs written segments, publishes the watermark
         std::atomic<int> m_error;
         bool m_wakeup;
@@ -145,6 +149,10 @@ class __attribute__((visibility("default"))) durable_log
         std::vector<uint32_t> m_lens;
         std::vector<uint32_t> m_crcs;
         std::vector<synced> m_pending;  // under m_mtx: at most one written, unsynced segment
+        std::vector<write_job*> m_jobs; // under m_mtx: at most one segment for the writer
+        unsigned char* m_spare;         // under m_mtx: the third staging arena, free (null:
+        bool m_spare_pinned;            //   the writer holds it)
+        bool m_stop_writer;             // under m_mtx: the destructor ends the writer thread
         bool m_stop;                    // under m_mtx: the destructor ends the sync thread
         std::atomic<uint32_t> m_fsync_delay_us;
         // bytes of frames staged outside the arenas (entries of more than

@@ -11,6 +11,14 @@
 // region the log is closed and replayed (a GPU-verified scan of both segment
 // files): every record must come back, in recno order, byte-exact.
 // Prints one JSON line.
+//
+// Engines of the flush thread's batch CRC: the GPU (default); with
+// REF_CRC_SO=path/to/oracle/_ref/libref_crc32c.so the reference
+// common/crc32c.cc itself (compiled unmodified, bench.py's CPU leg), called
+// per frame on the flush thread as the reference calls it per record
+// (txman/durable_log.cc:217-218) -- the same front-end with a CPU checksum,
+// timed in the same run.
+#include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -33,6 +41,17 @@ uint64_t splitmix64(uint64_t x)
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+typedef uint32_t (*ref_crc32c_fn)(uint32_t, const unsigned char*, size_t);
+ref_crc32c_fn g_ref = nullptr;
+
+int ref_batch(void*, const void* base, const uint64_t* off, const uint32_t* len, size_t n, uint64_t,
+              uint32_t* out)
+{
+    const unsigned char* b = static_cast<const unsigned char*>(base);
+    for (size_t i = 0; i < n; ++i) out[i] = g_ref(0, b + off[i], len[i]);
+    return 0;
 }
 
 double now()
@@ -97,7 +116,19 @@ int main(int argc, char** argv)
             entry_bytes += lens[t][k];
         }
 
+    const char* ref_so = getenv("REF_CRC_SO");
+    if (ref_so && *ref_so)
+    {
+        void* h = dlopen(ref_so, RTLD_NOW | RTLD_LOCAL);
+        g_ref = h ? reinterpret_cast<ref_crc32c_fn>(dlsym(h, "ref_crc32c")) : nullptr;
+        if (!g_ref)
+        {
+            fprintf(stderr, "REF_CRC_SO=%s: %s\n", ref_so, dlerror());
+            return 2;
+        }
+    }
     consus::durable_log log(seg);
+    if (g_ref) log.set_batch_crc_for_testing(ref_batch, nullptr);
     if (fake)
         log.set_batch_crc_for_testing(
             [](void*, const void*, const uint64_t*, const uint32_t*, size_t n, uint64_t,
@@ -193,7 +224,7 @@ int main(int argc, char** argv)
         &rp);
     log.close();
     const uint64_t frame_bytes = entry_bytes + total * 20;
-    printf("{\"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
+    printf("{\"engine\": \"%s\", \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
            "\"append_s\": %.6f, \"durable_s\": %.6f, \"appends_per_s\": %.1f, "
            "\"frame_GiB_per_s\": %.4f, \"flushes\": %llu, \"frames_flushed\": %llu, "
            "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
@@ -201,7 +232,8 @@ int main(int argc, char** argv)
            "\"patch\": %.4f, \"pwrite\": %.4f, \"fsync\": %.4f}, "
            "\"durable_latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, "
            "\"samples\": %zu}}\n",
-           threads, (unsigned long long)total, (unsigned long long)entry_bytes,
+           fake ? "none" : g_ref ? "reference-cpu" : "gpu", threads, (unsigned long long)total,
+           (unsigned long long)entry_bytes,
            (unsigned long long)frame_bytes, t_appended - t0, t_durable - t0,
            double(total) / (t_durable - t0), double(frame_bytes) / (t_durable - t0) / (1u << 30),
            (unsigned long long)flushes, (unsigned long long)frames,

@@ -24,7 +24,8 @@ while [ $# -gt 0 ]; do
     crossover) run crossover 400 python3 -u tools/varpath_crossover.py ;;
     rehearsal) run bench_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --share-device --steps 5 --warmup 2 --no-cpu ;;
-    dlog) run bench_dlog 300 python bench.py --config dlog --steps 30 ;;
+    dlog) run bench_dlog 400 python bench.py --config dlog --steps 30 ;;
+    latency) run latency_probe 300 env MI_CRC32C_GPU_MIN=0 python3 tools/latency_probe.py ;;
     zipf) run zipf_probe 300 python3 tools/zipf_probe.py ;;
     fixed) run fixed_probe 300 python3 tools/perf_probe.py ;;
     bench) run bench_default 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
