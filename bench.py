@@ -412,10 +412,11 @@ def run_dlog(args) -> dict:
                 "us_per_flush": {k: round(v / f * 1e6, 2) for k, v in x["flush_s"].items()}}
     best = median(runs["gpu"])
     pf = per_flush(best)
-    # the per-flush bound of the GPU batch: one launch-and-sync round trip
-    # (~13 us measured for an empty zero-copy launch)
+    # the per-flush bound of the GPU batch: the round trip of a one-frame batch
+    # through the same entry point (measured by dlog_bench before its run)
     # plus the flush's bytes at the host link's ~55 GB/s
-    bound = 13.0 + pf["frame_bytes_per_flush"] / 55e3
+    pf["empty_batch_us"] = best.get("empty_batch_us", 0.0)
+    bound = pf["empty_batch_us"] + pf["frame_bytes_per_flush"] / 55e3
     pf["batch_crc_bound_us"] = round(bound, 2)
     pf["batch_crc_vs_bound"] = round(pf["us_per_flush"]["batch_crc"] / bound, 3)
     cpu = None

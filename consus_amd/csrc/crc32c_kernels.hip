@@ -1347,7 +1347,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
     uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
     const uint32_t* __restrict__ pow2)
 {
-    stage_tables(tables);
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t li = lane_info();
     const uint64_t team = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kTeam;
@@ -1355,13 +1354,32 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
     const uint64_t team0 = team & ~uint64_t(7);  // first team of this wave
     const uint64_t iters = team0 < count ? (count - team0 + nteams - 1) / nteams : 0;
     const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
+    // the first record's offset and length are loaded before the table
+    // staging, so their latency (a PCIe round trip when they sit in mapped
+    // pinned memory: a durable-log flush) overlaps it
+    uint64_t nx_off = 0;
+    uint32_t nx_len = 0;
+    if (iters)
+    {
+        const uint64_t r0 = team < count ? team : count - 1;
+        nx_off = off[r0];
+        nx_len = team < count ? len[r0] : 0u;
+    }
+    stage_tables(tables);
     for (uint64_t it = 0; it < iters; ++it)
     {
         const uint64_t r_raw = team + it * nteams;
         const bool live = r_raw < count;
         const uint64_t r = live ? r_raw : count - 1;
-        const uint32_t L = live ? len[r] : 0u;
-        const uint64_t a = uint64_t(base) + off[r], E = a + L;
+        const uint32_t L = nx_len;
+        const uint64_t a = uint64_t(base) + nx_off, E = a + L;
+        if (it + 1 < iters)
+        {
+            const uint64_t rn_raw = r_raw + nteams;
+            const uint64_t rn = rn_raw < count ? rn_raw : count - 1;
+            nx_off = off[rn];
+            nx_len = rn_raw < count ? len[rn] : 0u;
+        }
         const uint64_t w0 = a & ~uint64_t(kRowBytes - 1);
         const uint64_t w1 = (E + kRowBytes - 1) & ~uint64_t(kRowBytes - 1);
         const uint32_t rows = uint32_t((w1 - w0) / kRowBytes);

@@ -628,17 +628,31 @@ int mi_crc32c_stream_sync(void)
 
 namespace mi_eng {
 
+// The usable (gfx950) devices, probed once per process: every multi-device
+// call (each durable-log flush) asks, and a property query per device per
+// call cost microseconds.
 int usable_devices(int* ordinals, int max)
 {
     if (fault_mode() == kFaultInit) return 0;
-    int n = 0, k = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess)
+    struct Found
     {
-        (void)hipGetLastError();
-        return 0;
-    }
-    for (int i = 0; i < n && i < kMaxDevices && k < max; ++i)
-        if (is_gfx950(i)) ordinals[k++] = i;
+        int n = 0;
+        int ord[kMaxDevices];
+    };
+    static const Found found = [] {
+        Found f;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess)
+        {
+            (void)hipGetLastError();
+            return f;
+        }
+        for (int i = 0; i < n && i < kMaxDevices; ++i)
+            if (is_gfx950(i)) f.ord[f.n++] = i;
+        return f;
+    }();
+    const int k = std::min(found.n, max);
+    for (int i = 0; i < k; ++i) ordinals[i] = found.ord[i];
     return k;
 }
 

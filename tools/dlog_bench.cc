@@ -31,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "consus_crc32c.h"
 #include "txman/durable_log.h"
 
 namespace {
@@ -125,6 +126,31 @@ int main(int argc, char** argv)
         {
             fprintf(stderr, "REF_CRC_SO=%s: %s\n", ref_so, dlerror());
             return 2;
+        }
+    }
+    // the floor of one flush's GPU batch: the round trip of a one-frame batch
+    // from mapped pinned memory through the log's engine entry point
+    double empty_us = 0;
+    if (!g_ref && !fake)
+    {
+        void* pin = nullptr;
+        if (mi_host_malloc_pinned(&pin, 4096) == MI_CRC32C_OK)
+        {
+            memset(pin, 7, 4096);
+            const uint64_t o = 0;
+            const uint32_t l = 64;
+            uint32_t c = 0;
+            std::vector<double> t;
+            for (int i = 0; i < 220; ++i)
+            {
+                const double a = now();
+                mi_crc32c_batch_multi(pin, &o, &l, nullptr, 1, 64, &c, MI_CRC32C_FALLBACK, nullptr,
+                                      0, 0);
+                if (i >= 20) t.push_back((now() - a) * 1e6);
+            }
+            std::sort(t.begin(), t.end());
+            empty_us = t[t.size() / 2];
+            mi_host_free_pinned(pin);
         }
     }
     consus::durable_log log(seg);
@@ -224,7 +250,7 @@ int main(int argc, char** argv)
         &rp);
     log.close();
     const uint64_t frame_bytes = entry_bytes + total * 20;
-    printf("{\"engine\": \"%s\", \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
+    printf("{\"engine\": \"%s\", \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
            "\"append_s\": %.6f, \"durable_s\": %.6f, \"appends_per_s\": %.1f, "
            "\"frame_GiB_per_s\": %.4f, \"flushes\": %llu, \"frames_flushed\": %llu, "
            "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
@@ -232,7 +258,8 @@ int main(int argc, char** argv)
            "\"patch\": %.4f, \"pwrite\": %.4f, \"fsync\": %.4f}, "
            "\"durable_latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, "
            "\"samples\": %zu}}\n",
-           fake ? "none" : g_ref ? "reference-cpu" : "gpu", threads, (unsigned long long)total,
+           fake ? "none" : g_ref ? "reference-cpu" : "gpu", empty_us, threads,
+           (unsigned long long)total,
            (unsigned long long)entry_bytes,
            (unsigned long long)frame_bytes, t_appended - t0, t_durable - t0,
            double(total) / (t_durable - t0), double(frame_bytes) / (t_durable - t0) / (1u << 30),

@@ -21,6 +21,7 @@ while [ $# -gt 0 ]; do
     tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
+    flush) run flush_probe 300 ./tools/flush_probe 1000 ;;
     crossover) run crossover 400 python3 -u tools/varpath_crossover.py ;;
     rehearsal) run bench_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --share-device --steps 5 --warmup 2 --no-cpu ;;
@@ -37,6 +38,12 @@ while [ $# -gt 0 ]; do
                [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
                echo -n "round $rnd short=$v class=$m "; env $envs timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
              done; done | tee "$OUT/shortiso.out"; set -- ;;
+    zipfpmc) C="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+             for m in full keep drop; do
+               envs="ZIPF_WARM=2 ZIPF_ROUNDS=1"; [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
+               (cd /tmp && env $envs timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$m" -o k -- python3 "$ROOT/tools/zipf_probe.py" > "$OUT/pmc_$m.log" 2>&1) || { tail -5 "$OUT/pmc_$m.log"; exit 1; }
+               echo "== $m"; python3 tools/pmc_summary.py "$OUT/pmc_$m" crc32c_sorted_kernel sorted_cost_kernel
+             done | tee "$OUT/zipfpmc.out" ;;
     sorted) run pytest_sorted 600 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread ;;
     ab) AB_ROUNDS=${AB_ROUNDS:-3} run ab 900 python3 -u tools/ab.py --zipf "$@"; break ;;
     abfixed) AB_ROUNDS=${AB_ROUNDS:-3} run abfixed 900 python3 -u tools/ab.py "$@"; break ;;

@@ -32,11 +32,12 @@ d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer
 d_off.upload(off)
 d_len.upload(ln)
 hint = int(ln.sum(dtype=np.uint64))
-for _ in range(100):
+WARM, ROUNDS = int(os.environ.get("ZIPF_WARM", "100")), int(os.environ.get("ZIPF_ROUNDS", "5"))
+for _ in range(WARM):
     E.device_batch(data, d_off, d_len, R, out, total_bytes=hint, asynchronous=True)
 E.sync()
 rounds = []
-for _ in range(5):
+for _ in range(ROUNDS):
     E.timer_start()
     for _ in range(50):
         E.device_batch(data, d_off, d_len, R, out, total_bytes=hint, asynchronous=True)
