@@ -36,9 +36,11 @@ constexpr int kTabZero = kTabZInv128 + 1024;    // 4 zero words (init 0 when ini
 constexpr int kTabFInit = kTabZero + 4;         // Z_n(0xFFFFFFFF), n = 0..4096 (init 0 seeds)
 constexpr int kTabZRows = kTabFInit + 4100;     // G^{128 k}, k = 1..32 (last-piece shifts)
 constexpr int kTabZNeg = kTabZRows + 32 * 1024; // Z_{-m} = (Z_m)^{-1}, m = 0..127 (direct kernel)
-constexpr int kTabLane = kTabZNeg + 128 * 1024; // Z_16, Z_12, Z_8, Z_4, Z_32, Z_64 as six 64-entry
-                                                 // tables each: [op][c][i] = Z(i << 6c) (lane fold)
-constexpr int kTabWords = kTabLane + 6 * 6 * 64;
+constexpr int kTabLane = kTabZNeg + 128 * 1024; // Z_16, Z_12, Z_8, Z_4, Z_32, Z_64, Z_128 as six
+                                                 // 64-entry tables each: [op][c][i] = Z(i << 6c)
+                                                 // (lane fold; Z_128: the LDS-free row update)
+constexpr int kLaneOps = 7;
+constexpr int kTabWords = kTabLane + kLaneOps * 6 * 64;
 
 // LDS image of the record kernels (bytes).
 constexpr uint32_t kLdsMain = 0;            // 128 KiB bank-private G^{128}
@@ -85,10 +87,24 @@ constexpr uint64_t kDirectMaxCount = 1u << 18;   // records
 constexpr uint64_t kDirectMaxBytes = 32ull << 20;  // sum of lengths
 constexpr uint64_t kDirectMaxRecord = 16u << 10;   // longest record (128 rows for one team;
                                                    // the planned path wins above ~32 KiB)
+// Batches of at most kLiteMaxBytes (a durable-log flush) take the LDS-free
+// form: 256-thread workgroups, no 152 KiB table staging.
+constexpr uint64_t kLiteMaxBytes = 2ull << 20;
+constexpr int kLiteBlock = 256;
+// Completion word: when `signal` is set, the last workgroup to finish stores
+// `seq` to signal->flag (mapped host memory) after every CRC is visible
+// system-wide, so the host may spin on it instead of a stream sync.
+struct DoneSignal
+{
+    uint32_t* counter;  // device word, 0 between launches
+    uint32_t* flag;     // mapped pinned host word (device address)
+    uint32_t seq;
+};
 hipError_t launch_direct(const void* base, const uint64_t* offsets, const uint32_t* lengths,
-                         const uint32_t* inits, uint64_t count, uint32_t* out,
+                         const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
                          const uint32_t* tables, const uint32_t* pow2, int grid,
-                         hipStream_t stream);
+                         hipStream_t stream, const DoneSignal* signal = nullptr,
+                         int lite = -1);  // -1: by size; 0 / 1: force (tests)
 
 // force_scan: run the separate scan pass even for plans that do not need it
 // (MI_CRC32C_PLAN_SCAN=1, so the tests cover both plan forms).

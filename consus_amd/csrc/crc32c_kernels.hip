@@ -184,13 +184,15 @@ __device__ __forceinline__ uint32_t team_fold(const uint32_t (&V)[4])
 // 7:2 only, so each slice's address is one shift.  Costs 36 VGPRs.
 struct LaneTabs
 {
-    uint32_t t[36];
+    uint32_t t[6 * kLaneOps];
 };
+// the first N of the 42 (36: the fold's six operators; 42: and Z_128)
+template <int N = 36>
 __device__ __forceinline__ void load_lane_tabs(LaneTabs& L, const uint32_t* __restrict__ tables)
 {
     const uint32_t* p = tables + kTabLane + (threadIdx.x & 63u);
 #pragma unroll
-    for (int k = 0; k < 36; ++k) L.t[k] = p[k * 64];
+    for (int k = 0; k < N; ++k) L.t[k] = p[k * 64];
 }
 __device__ __forceinline__ uint32_t bperm(uint32_t addr, uint32_t tab)
 {
@@ -211,6 +213,21 @@ __device__ __forceinline__ uint32_t team_fold_lane(const uint32_t (&V)[4], const
     const uint32_t y = zL<0>(L, x) ^ from_lane_up<1>(x);
     const uint32_t w = zL<4>(L, y) ^ from_lane_up<2>(y);
     return zL<5>(L, w) ^ from_lane_up<4>(w);
+}
+
+// The row update through the Z_128 lane tables (no LDS image): six
+// permutes per chain instead of four bank-private lookups.  Wave-uniform
+// control flow only (inactive lanes would read as 0); `act` keeps the chains
+// of a team whose record has ended, `first` starts them.
+__device__ __forceinline__ void row_update_lane(uint32_t (&V)[4], const uint4 d, const LaneTabs& L,
+                                                bool act, bool first)
+{
+    const uint32_t n0 = zL<6>(L, V[0]) ^ d.x, n1 = zL<6>(L, V[1]) ^ d.y;
+    const uint32_t n2 = zL<6>(L, V[2]) ^ d.z, n3 = zL<6>(L, V[3]) ^ d.w;
+    V[0] = act ? (first ? d.x : n0) : V[0];
+    V[1] = act ? (first ? d.y : n1) : V[1];
+    V[2] = act ? (first ? d.z : n2) : V[2];
+    V[3] = act ? (first ? d.w : n3) : V[3];
 }
 
 // Record bytes are read exactly once: non-temporal loads (global_load_dwordx4
@@ -1341,16 +1358,23 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
 // by the row update and team fold of the fixed kernel, and finished with the
 // seed: crc = ~(Z_L(~init) ^ raw).  Rows go 8 at a time (one load group).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
+// LITE (batches up to kLiteMaxBytes): 256-thread workgroups, no LDS; the
+// row update and the fold go through the lane tables (row_update_lane,
+// team_fold_lane), 42 VGPRs loaded from L2 beside the first record's reads,
+// instead of a 152 KiB LDS image staged by every workgroup before any
+// record is read.  Same rows, masks and finish.
+template <bool LITE>
+__global__ __launch_bounds__(LITE ? kLiteBlock : kBlock, 1) void crc32c_direct_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
-    const uint32_t* __restrict__ pow2)
+    const uint32_t* __restrict__ pow2, DoneSignal sig)
 {
+    constexpr int B = LITE ? kLiteBlock : kBlock;
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t li = lane_info();
-    const uint64_t team = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kTeam;
-    const uint64_t nteams = uint64_t(gridDim.x) * kBlock / kTeam;
+    const uint64_t team = (uint64_t(blockIdx.x) * B + threadIdx.x) / kTeam;
+    const uint64_t nteams = uint64_t(gridDim.x) * B / kTeam;
     const uint64_t team0 = team & ~uint64_t(7);  // first team of this wave
     const uint64_t iters = team0 < count ? (count - team0 + nteams - 1) / nteams : 0;
     const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
@@ -1365,7 +1389,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
         nx_off = off[r0];
         nx_len = team < count ? len[r0] : 0u;
     }
-    stage_tables(tables);
+    LaneTabs lt;
+    if constexpr (LITE)
+        load_lane_tabs<6 * kLaneOps>(lt, tables);
+    else
+        stage_tables(tables);
     for (uint64_t it = 0; it < iters; ++it)
     {
         const uint64_t r_raw = team + it * nteams;
@@ -1387,8 +1415,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
         // folded.  The wave runs as many groups as its longest record needs;
         // rows past a record's end load a zero block and are not folded, so
         // every load is unconditional and the vmcnt counts stay exact.
-        uint32_t ngw = (rows + kGroupRows - 1) / kGroupRows;
-        for (int dlt = 32; dlt >= 1; dlt >>= 1) ngw = max(ngw, uint32_t(__shfl_xor(int(ngw), dlt)));
+        uint32_t rmax = rows;
+        for (int dlt = 32; dlt >= 1; dlt >>= 1) rmax = max(rmax, uint32_t(__shfl_xor(int(rmax), dlt)));
+        const uint32_t ngw = (rmax + kGroupRows - 1) / kGroupRows;
         auto load_group = [&](uint4 (&buf)[kGroupRows], uint32_t g) {
 #pragma unroll
             for (int k = 0; k < kGroupRows; ++k)
@@ -1408,14 +1437,25 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
             for (int k = 0; k < kGroupRows; ++k)
             {
                 const uint32_t row = g * kGroupRows + k;
-                if (row >= rows) break;
-                uint4 d = buf[k];
-                if (row == 0) d = mask_from(d, f0);
-                if (row + 1 == rows) d = mask_below(d, bl);
-                if (row == 0)
-                    row_first(V, d);
+                if constexpr (LITE)
+                {
+                    if (row >= rmax) break;  // wave-uniform
+                    uint4 d = buf[k];
+                    if (row == 0) d = mask_from(d, f0);
+                    if (row + 1 == rows) d = mask_below(d, bl);
+                    row_update_lane(V, d, lt, row < rows, row == 0);
+                }
                 else
-                    row_update(V, d, li);
+                {
+                    if (row >= rows) break;
+                    uint4 d = buf[k];
+                    if (row == 0) d = mask_from(d, f0);
+                    if (row + 1 == rows) d = mask_below(d, bl);
+                    if (row == 0)
+                        row_first(V, d);
+                    else
+                        row_update(V, d, li);
+                }
             }
         };
         uint4 A[kGroupRows], B[kGroupRows];
@@ -1429,7 +1469,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
             __builtin_amdgcn_sched_barrier(0);
             fold_group(B, g + 1);
         }
-        const uint32_t W = team_fold(V);  // every lane of the wave takes part
+        uint32_t W;  // every lane of the wave takes part
+        if constexpr (LITE)
+            W = team_fold_lane(V, lt);
+        else
+            W = team_fold(V);
         if (tl == 0 && live)
         {
             const uint32_t raw = zglob(tables + kTabZNeg + uint32_t(w1 - E) * 1024, W);
@@ -1447,19 +1491,44 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_direct_kernel(
             out[r] = ~(seed ^ raw);
         }
     }
+    if (sig.counter)
+    {
+        // each thread's CRC stores reach the system before its workgroup
+        // counts itself done; the last one to count publishes seq
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0 && atomicAdd(sig.counter, 1u) == gridDim.x - 1)
+        {
+            atomicExch(sig.counter, 0u);  // ready for the next launch on the stream
+            __threadfence_system();
+            *reinterpret_cast<volatile uint32_t*>(sig.flag) = sig.seq;
+        }
+    }
 }
 
 hipError_t launch_direct(const void* base, const uint64_t* offsets, const uint32_t* lengths,
-                         const uint32_t* inits, uint64_t count, uint32_t* out,
+                         const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
                          const uint32_t* tables, const uint32_t* pow2, int grid,
-                         hipStream_t stream)
+                         hipStream_t stream, const DoneSignal* signal, int lite)
 {
     if (count == 0) return hipSuccess;
+    const DoneSignal sig = signal ? *signal : DoneSignal{nullptr, nullptr, 0};
+    if (lite < 0) lite = total_bytes <= kLiteMaxBytes;
+    if (lite)
+    {
+        // 32 teams per workgroup; up to 4 workgroups per CU
+        const uint64_t need = (count + (kLiteBlock / kTeam) - 1) / (kLiteBlock / kTeam);
+        const uint64_t g = std::min<uint64_t>(need, uint64_t(grid) * 4);
+        hipLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(uint32_t(g)), dim3(kLiteBlock), 0, stream,
+                           static_cast<const uint8_t*>(base), offsets, lengths, inits, count, out,
+                           tables, pow2, sig);
+        return hipGetLastError();
+    }
     const uint64_t need = (count + (kBlock / kTeam) - 1) / (kBlock / kTeam);
     if (uint64_t(grid) > need) grid = int(need);
-    hipLaunchKernelGGL(crc32c_direct_kernel, dim3(grid), dim3(kBlock), kLdsBytes, stream,
+    hipLaunchKernelGGL(crc32c_direct_kernel<false>, dim3(grid), dim3(kBlock), kLdsBytes, stream,
                        static_cast<const uint8_t*>(base), offsets, lengths, inits, count, out,
-                       tables, pow2);
+                       tables, pow2, sig);
     return hipGetLastError();
 }
 
@@ -2592,7 +2661,7 @@ hipError_t configure_kernels()
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_chunk_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (e == hipSuccess)
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_direct_kernel),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_direct_kernel<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),

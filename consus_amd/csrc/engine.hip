@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,6 +46,18 @@ namespace {
 constexpr uint64_t kPackMax = uint64_t(4) << 20;
 constexpr uint64_t kPackInPlace = uint64_t(512) << 10;
 constexpr uint64_t kZeroCopyMax = uint64_t(8) << 10;  // packed inputs read in place by the GPU
+// completion word of synchronous direct launches: pin_small word, and how
+// long the host spins on it before it blocks in a stream sync
+constexpr int kDoneWord = 16;
+constexpr int kDoneSpinUs = 1000;
+
+// MI_CRC32C_DONE_WORD=0: synchronous direct launches wait in a stream sync
+// instead of spinning on their completion word (A/B; read per batch).
+bool done_word_disabled()
+{
+    const char* e = std::getenv("MI_CRC32C_DONE_WORD");
+    return e && !std::strcmp(e, "0");
+}
 // Device buffers from this size take launch_single (fixed-record kernel on
 // the 4 KiB chunks + a two-level combine tree) instead of the variable path.
 constexpr uint64_t kSingleMin = 64 * 1024;
@@ -148,8 +161,8 @@ int build_device(int device)
     }
     {
         // lane-fold tables: 6-bit slices of the team fold's six shifts (chunk 5 holds bits 30-31)
-        const uint64_t shifts[6] = {16, 12, 8, 4, 32, 64};
-        for (int k = 0; k < 6; ++k)
+        const uint64_t shifts[kLaneOps] = {16, 12, 8, 4, 32, 64, kRowBytes};
+        for (int k = 0; k < kLaneOps; ++k)
         {
             const Op32 z = zeros_op(shifts[k]);
             for (int c = 0; c < 6; ++c)
@@ -304,7 +317,9 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
-    PinBuf pin_small;                   // plan-size read-back, small host outputs
+    DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
+    uint32_t done_seq = 0;
+    PinBuf pin_small;                   // plan-size read-back; word kDoneWord: completion word
     PinBuf pin_stage, pin_out;          // packed small host batches: inputs, CRCs
     int ordinal = -1;
     // set by the last device batch: where its overflow shows when a caller's
@@ -322,7 +337,47 @@ struct Ctx
         HIP_TRY(hipEventCreate(&ev0));
         HIP_TRY(hipEventCreate(&ev1));
         HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        int st;
+        if ((st = done_ctr.reserve(64))) return st;
+        HIP_TRY(hipMemset(done_ctr.p, 0, 64));
         return pin_small.reserve(4096);
+    }
+    // The completion word of the next synchronous direct launch (nullptr: the
+    // pinned page has no device mapping; then the caller syncs the stream).
+    bool next_signal(DoneSignal* s)
+    {
+        if (!pin_small.dev || !done_ctr.p || done_word_disabled()) return false;
+        volatile uint32_t* h = pin_small.as<uint32_t>() + kDoneWord;
+        *h = 0;
+        if (++done_seq == 0) done_seq = 1;
+        *s = DoneSignal{done_ctr.as<uint32_t>(), static_cast<uint32_t*>(pin_small.dev) + kDoneWord,
+                        done_seq};
+        return true;
+    }
+    // Wait for the launch that carries `s` (or, without one, the stream):
+    // spin on the completion word for up to kDoneSpinUs, then block in a stream
+    // sync, which also reports any fault of the launch.
+    int wait_direct(bool signalled)
+    {
+        if (signalled)
+        {
+            const volatile uint32_t* h = pin_small.as<uint32_t>() + kDoneWord;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t n = 0;; ++n)
+            {
+                if (*h == done_seq)
+                {
+                    std::atomic_thread_fence(std::memory_order_acquire);
+                    return MI_CRC32C_OK;
+                }
+                __builtin_ia32_pause();
+                if ((n & 255u) == 255u &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kDoneSpinUs))
+                    break;
+            }
+        }
+        HIP_TRY(hipStreamSynchronize(stream));
+        return MI_CRC32C_OK;
     }
     // Waits for the stream's work, then frees every buffer, event and the stream.
     void release()
@@ -330,7 +385,7 @@ struct Ctx
         if (stream) (void)hipStreamSynchronize(stream);
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs, &srt_cost,
-                          &srt_ctrl, &srt_items})
+                          &srt_ctrl, &srt_items, &done_ctr})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -482,6 +537,15 @@ bool zero_copy_disabled()
     return e && !std::strcmp(e, "0");
 }
 
+// MI_CRC32C_DIRECT_LITE=0 / 1: the direct kernel's LDS-free form never /
+// always (tests cover both; default: by size, kLiteMaxBytes).  Read per batch.
+int direct_lite_mode()
+{
+    const char* e = std::getenv("MI_CRC32C_DIRECT_LITE");
+    if (!e || !*e) return -1;
+    return std::strcmp(e, "0") ? 1 : 0;
+}
+
 // MI_CRC32C_PLAN_SCAN=1: plans always take the separate scan pass (which
 // only plans of more than 16M records need), so tests exercise both forms.
 bool plan_scan_forced()
@@ -510,8 +574,8 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
     // when the longest record is known to be short
     if (max_len <= kDirectMaxRecord && total_bytes <= kDirectMaxBytes && count <= kDirectMaxCount)
     {
-        HIP_TRY(launch_direct(base, off, len, inits, count, out, d->d_tables, d->d_pow2, d->cus,
-                              c->stream));
+        HIP_TRY(launch_direct(base, off, len, inits, count, total_bytes, out, d->d_tables,
+                              d->d_pow2, d->cus, c->stream, nullptr, direct_lite_mode()));
         return MI_CRC32C_OK;
     }
     if (total_bytes && count < kSortedMaxCount && varpath_forced() != 1 &&
@@ -726,13 +790,16 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
                 std::memcpy(hp + count * 8, lengths, count * 4);
                 if (inits) std::memcpy(hp + count * 12, inits, count * 4);
                 const uint8_t* sp = static_cast<const uint8_t*>(c->pin_stage.dev);
+                DoneSignal sig;
+                const bool signalled = c->next_signal(&sig);
                 HIP_TRY(launch_direct(zsrc, reinterpret_cast<const uint64_t*>(sp),
                                       reinterpret_cast<const uint32_t*>(sp + count * 8),
                                       inits ? reinterpret_cast<const uint32_t*>(sp + count * 12)
                                             : nullptr,
-                                      count, static_cast<uint32_t*>(c->pin_out.dev), d->d_tables,
-                                      d->d_pow2, d->cus, c->stream));
-                HIP_TRY(hipStreamSynchronize(c->stream));
+                                      count, total, static_cast<uint32_t*>(c->pin_out.dev),
+                                      d->d_tables, d->d_pow2, d->cus, c->stream,
+                                      signalled ? &sig : nullptr, direct_lite_mode()));
+                if ((st = c->wait_direct(signalled))) return st;
                 std::memcpy(out, c->pin_out.p, count * 4);
                 mi_host::note_zero_copy_batch();
                 return MI_CRC32C_OK;
@@ -772,13 +839,16 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
             c->pin_stage.dev && c->pin_out.dev)
         {
             const uint8_t* sp = static_cast<const uint8_t*>(c->pin_stage.dev);
+            DoneSignal sig;
+            const bool signalled = c->next_signal(&sig);
             HIP_TRY(launch_direct(sp + data_at, reinterpret_cast<const uint64_t*>(sp),
                                   reinterpret_cast<const uint32_t*>(sp + count * 8),
                                   inits ? reinterpret_cast<const uint32_t*>(sp + count * 12)
                                         : nullptr,
-                                  count, static_cast<uint32_t*>(c->pin_out.dev), d->d_tables,
-                                  d->d_pow2, d->cus, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
+                                  count, total, static_cast<uint32_t*>(c->pin_out.dev),
+                                  d->d_tables, d->d_pow2, d->cus, c->stream,
+                                  signalled ? &sig : nullptr, direct_lite_mode()));
+            if ((st = c->wait_direct(signalled))) return st;
             std::memcpy(out, c->pin_out.p, count * 4);
             return MI_CRC32C_OK;
         }

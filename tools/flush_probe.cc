@@ -7,8 +7,10 @@
 //
 // Columns: frames and bytes per flush; us per call of mi_crc32c_batch_multi
 // (the log's default engine), of mi_crc32c_batch, of the same batch staged
-// by copy commands (MI_CRC32C_ZERO_COPY=0), of an empty-kernel round trip
-// (one 16-B record), and the bound 'round trip + bytes / 55 GB/s'.
+// by copy commands (MI_CRC32C_ZERO_COPY=0), of the direct kernel with its LDS
+// table image (MI_CRC32C_DIRECT_LITE=0), of the default form waited for by a
+// stream sync (MI_CRC32C_DONE_WORD=0), of a one-record round trip (16 B),
+// and the bound 'round trip + bytes / 55 GB/s'.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -58,9 +60,9 @@ int main(int argc, char** argv)
         x ^= x << 13, x ^= x >> 7, x ^= x << 17;
         arena[i] = (unsigned char)x;
     }
-    printf("%7s %9s %10s %10s %10s %10s %10s\n", "frames", "bytes", "multi_us", "batch_us",
-           "copy_us", "empty_us", "bound_us");
-    for (size_t frames : {16, 64, 128, 270, 512, 1024, 2048, 4096})
+    printf("%7s %9s %10s %10s %10s %10s %10s %10s %10s\n", "frames", "bytes", "multi_us",
+           "batch_us", "copy_us", "lds_us", "sync_us", "empty_us", "bound_us");
+    for (size_t frames : {1, 16, 64, 128, 270, 512, 1024, 2048, 4096, 8192})
     {
         std::vector<uint64_t> off(frames);
         std::vector<uint32_t> len(frames);
@@ -91,14 +93,29 @@ int main(int argc, char** argv)
         });
         unsetenv("MI_CRC32C_ZERO_COPY");
         if (memcmp(out.data(), out2.data(), frames * 4)) printf("MISMATCH copy\n");
+        setenv("MI_CRC32C_DIRECT_LITE", "0", 1);
+        const double lds = median_us(reps, [&] {
+            mi_crc32c_batch(arena, off.data(), len.data(), nullptr, frames, total, out2.data(),
+                            MI_CRC32C_FALLBACK);
+        });
+        unsetenv("MI_CRC32C_DIRECT_LITE");
+        if (memcmp(out.data(), out2.data(), frames * 4)) printf("MISMATCH lds\n");
+        setenv("MI_CRC32C_DONE_WORD", "0", 1);
+        const double sync = median_us(reps, [&] {
+            mi_crc32c_batch(arena, off.data(), len.data(), nullptr, frames, total, out2.data(),
+                            MI_CRC32C_FALLBACK);
+        });
+        unsetenv("MI_CRC32C_DONE_WORD");
+        if (memcmp(out.data(), out2.data(), frames * 4)) printf("MISMATCH sync\n");
         const uint64_t o16 = 0;
         const uint32_t l16 = 16;
         uint32_t c16 = 0;
         const double empty = median_us(reps, [&] {
             mi_crc32c_batch(arena, &o16, &l16, nullptr, 1, 16, &c16, MI_CRC32C_FALLBACK);
         });
-        printf("%7zu %9llu %10.2f %10.2f %10.2f %10.2f %10.2f\n", frames, (unsigned long long)at,
-               multi, batch, copy, empty, empty + double(at) / 55e3);
+        printf("%7zu %9llu %10.2f %10.2f %10.2f %10.2f %10.2f %10.2f %10.2f\n", frames,
+               (unsigned long long)at, multi, batch, copy, lds, sync, empty,
+               empty + double(at) / 55e3);
         fflush(stdout);
     }
     mi_crc32c_stats_t st;

@@ -22,7 +22,12 @@ while [ $# -gt 0 ]; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
     flush) run flush_probe 300 ./tools/flush_probe 1000 ;;
+    launch) run launch_probe 120 ./tools/launch_probe 2000 && run launch_probe_spin 120 ./tools/launch_probe 2000 spin ;;
     crossover) run crossover 400 python3 -u tools/varpath_crossover.py ;;
+    varprof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/varprof" -o k -- python3 "$ROOT/tools/varpath_crossover.py" --reps 10 > "$OUT/varprof.log" 2>&1) || { tail -20 "$OUT/varprof.log"; exit 1; }
+             C="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+             (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/varpmc" -o k -- python3 "$ROOT/tools/varpath_crossover.py" --reps 3 > "$OUT/varpmc.log" 2>&1) || { tail -20 "$OUT/varpmc.log"; exit 1; }
+             python3 tools/pmc_summary.py "$OUT/varpmc" crc32c_chunk_kernel crc32c_finalize_kernel crc32c_direct_kernel plan_ sorted_ | tee "$OUT/varpmc.out" ;;
     rehearsal) run bench_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --share-device --steps 5 --warmup 2 --no-cpu ;;
     dlog) run bench_dlog 400 python bench.py --config dlog --steps 30 ;;
@@ -44,6 +49,7 @@ while [ $# -gt 0 ]; do
                (cd /tmp && env $envs timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$m" -o k -- python3 "$ROOT/tools/zipf_probe.py" > "$OUT/pmc_$m.log" 2>&1) || { tail -5 "$OUT/pmc_$m.log"; exit 1; }
                echo "== $m"; python3 tools/pmc_summary.py "$OUT/pmc_$m" crc32c_sorted_kernel sorted_cost_kernel
              done | tee "$OUT/zipfpmc.out" ;;
+    direct) run pytest_direct 400 python -u -m pytest tests/test_gpu_direct.py tests/test_gpu_parity.py tests/test_durable_log.py -x -q --timeout 120 --timeout-method thread ;;
     sorted) run pytest_sorted 600 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread ;;
     ab) AB_ROUNDS=${AB_ROUNDS:-3} run ab 900 python3 -u tools/ab.py --zipf "$@"; break ;;
     abfixed) AB_ROUNDS=${AB_ROUNDS:-3} run abfixed 900 python3 -u tools/ab.py "$@"; break ;;
