@@ -1827,14 +1827,13 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
 constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
 constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 1;  // rows of the largest item (513)
 constexpr uint32_t kSortBins = kSortRows;                         // bin = kSortRows - rows
-// rows per ring of the sorted kernel (2 or 4)
-#ifndef MI_SORT_RING
-#define MI_SORT_RING 2
-#endif
+// rows per ring of the sorted kernel (4 measured slower: profiles/r03_sorted_wave_roles_ab.txt)
+constexpr int kSortRing = 2;
 // XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
-// and in every timeline measured (tools/sorted_stamps.py, 5 GPU sessions)
+// and in every timeline measured (round 2's stamped builds, 5 GPU sessions,
+// profiles/r02_sorted_stamps_timeline.txt)
 // the odd XCDs finished configs[2] 10-30 us after the even ones with equal
-// shares.  Even workgroups take MI_SORT_XCDW/1000 more cost, odd ones as much
+// shares.  Even workgroups take kSortXcdw/1000 more cost, odd ones as much
 // less (A/B against equal shares: 0.878-0.905 ms vs 0.885-0.916 at 20;
 // 15 is the default, 0 turns it off).
 constexpr uint32_t kSortXcdw = 15;
@@ -1845,16 +1844,6 @@ constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a s
 constexpr uint32_t kSortFirst = 0x40000000u;  // ... its first piece (carries the init)
 constexpr uint32_t kSortRecMask = 0x3FFFFFFFu;
 constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
-
-// measurement builds only: MI_SORT_STAMP=1 (2: slots 6 and 7 = the wave's
-// first group of <= 8 and of <= 2 rows) records s_memrealtime stamps
-// (100 MHz) per wave into the item workspace past item_cap, 8 words: start,
-// end of the prologue, end of the last group, then after the table staging,
-// the block search, the boundaries, binning pass 1 and the item allocation
-// (tools/sorted_stamps.py)
-#ifndef MI_SORT_STAMP
-#define MI_SORT_STAMP 0
-#endif
 
 uint32_t sorted_blocks(uint64_t count) { return uint32_t((count + kSortRecs - 1) / kSortRecs); }
 
@@ -2218,27 +2207,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint32_t lane = threadIdx.x & 63u;
-    uint64_t* const stamps = reinterpret_cast<uint64_t*>(items + item_cap) +
-                             (uint64_t(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64) * 8;
-    if (MI_SORT_STAMP && lane == 0)
-    {
-        stamps[0] = __builtin_amdgcn_s_memrealtime();
-        stamps[6] = 0;
-        stamps[7] = 0;
-    }
     if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = 0;
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     stage_tables(tables);  // ends with a barrier
-    if (MI_SORT_STAMP && lane == 0) stamps[3] = __builtin_amdgcn_s_memrealtime();
 
     // (1) Wave 0: the two targets and the cost blocks holding them.
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
-    if (MI_SORT_STAMP && lane == 0) stamps[4] = __builtin_amdgcn_s_memrealtime();
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S);
-    if (MI_SORT_STAMP && lane == 0) stamps[5] = __builtin_amdgcn_s_memrealtime();
 
     // (3) Bin the items by row count, largest first.  Whole records and the
     // last pieces of split records go to this workgroup's slots of the
@@ -2341,7 +2319,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     pass(false);
     __syncthreads();
-    if (MI_SORT_STAMP == 1 && lane == 0) stamps[6] = __builtin_amdgcn_s_memrealtime();
     {
         const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
         uint64_t total;
@@ -2369,7 +2346,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         }
     }
     __syncthreads();
-    if (MI_SORT_STAMP == 1 && lane == 0) stamps[7] = __builtin_amdgcn_s_memrealtime();
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     if (n_items)
     {
@@ -2397,7 +2373,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     __syncthreads();
     if (n_items == 0) return;
 
-    if (MI_SORT_STAMP && lane == 0) stamps[1] = __builtin_amdgcn_s_memrealtime();
     // (4) Groups of 8 items, largest first, one LDS grab per group.
     const uint32_t n_groups = (n_items + 7) / 8;
     const uint32_t tl = threadIdx.x & (kTeam - 1);
@@ -2470,7 +2445,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             rmax = t <= tlast ? max(rmax, x) : rmax;
             rmin = t <= tlast ? min(rmin, x) : rmin;
         }
-        s.n = (rmax + MI_SORT_RING - 1) & ~(MI_SORT_RING - 1);
+        s.n = (rmax + kSortRing - 1) & ~(kSortRing - 1);
         s.fmin = s.n - rmax;
         s.fedge = s.n - rmin + 1;
         s.fast = tlast == 7 ? s.fedge + 1 : s.n;
@@ -2494,23 +2469,23 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // Row ring of RB buffers: row r of a group sits in b[r % RB]; each row
     // step issues row r + RB - 1 (this group's, or one of the next group's
     // first rows) before folding row r.  Groups are padded to a multiple of
-    // RB rows, so the roles never change.  RB = 2 (MI_SORT_RING): one row in
+    // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
     // flight per wave while another folds (measured on the headline batch:
     // one row ahead costs < 1 % against three; here it keeps the padding to
     // half a row per group).
-    constexpr int RB = MI_SORT_RING;
+    constexpr int RB = kSortRing;
     uint4 b[RB];
 #pragma unroll
     for (int j = 0; j < RB - 1; ++j) b[j] = load16(row_ptr(cur0, j, false));
     __builtin_amdgcn_sched_barrier(0);
     // One group: hash `cur` (shape sh) while the next group's view is built
     // into `nxt`.  The loop runs it twice per iteration with the two views
-    // swapped (MI_SORT_PINGPONG), so the ~20 registers of a view are never
+    // swapped (round 2 A/B: profiles/r02_sorted_view32_pingpong_ab.txt), so the ~20 registers of a view are never
     // copied at the back edge.
     auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
         // A 2-row group runs no body loop, so its last row can be issued now,
         // a whole group header ahead of its folding, instead of one row
-        // ahead (MI_SORT_SHORTPRE); b[1] is free here.
+        // ahead (round 2 A/B: profiles/r02_sorted_shortpre_ab.txt); b[1] is free here.
         const bool pre = RB == 2 && sh.n == 2;
         if (pre) b[1] = load16(row_ptr(cur, 1, false));
         const uint32_t g_nn = grab();
@@ -2519,13 +2494,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         nxt = sort_view(d_nxt, shn.n, tl, inits, zero_word, ones_word);
         uint32_t V[4] = {0, 0, 0, 0};
         const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
-        if (MI_SORT_STAMP == 2 && lane == 0)
-        {
-            // the wave's first group of <= 8 rows (slot 6) and of <= 2 rows (slot 7)
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (n <= 8 && stamps[6] == 0) stamps[6] = now;
-            if (n <= 2 && stamps[7] == 0) stamps[7] = now;
-        }
         // General row: padding skip, start mask and init word (rows up to
         // fedge), end mask (row n - 1), zero-block reads.  Used for the first
         // rows and the last RB of a group; the rows between take the body
@@ -2617,7 +2585,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
-    if (MI_SORT_STAMP && lane == 0) stamps[2] = __builtin_amdgcn_s_memrealtime();
 }
 
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,
