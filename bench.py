@@ -265,6 +265,22 @@ def rccl_gather(E, dist, rank: int, world: int, out, R: int, digests, rec) -> di
     return res
 
 
+def multi_rank_fields(rec: dict, ranks: list, gather, world: int, share_device: bool) -> int:
+    """The N > 1 keys of the bench line: every rank's identity (rank, HIP
+    device, PCI bus id, per-launch ms), the count of distinct GPUs, the RCCL
+    gather's result and its communicator's rank count.  Returns the exit code:
+    4 when the gather failed or did not verify, or when the ranks did not land
+    on `world` distinct GPUs (outside a one-GPU rehearsal) -- the line says
+    what, the exit code makes it fail (tests/test_bench_shape.py)."""
+    rec["ranks"] = ranks
+    rec["distinct_gpus"] = len({r["pci_bus_id"] for r in ranks})
+    rec["gather"] = gather
+    rec["rccl_ranks"] = gather.get("rccl_ranks") if gather else None
+    bad = bool((gather or {}).get("error")) or (gather is not None and rec["rccl_ranks"] != world) \
+        or (not share_device and rec["distinct_gpus"] != world)
+    return 4 if bad else 0
+
+
 def rank_identity(E, dist, rank: int, device: int, launch_ms: float) -> list | None:
     """Every rank's (rank, HIP device, PCI bus id, per-launch ms), gathered on
     the gloo control plane: the line shows which physical GPUs ran."""
@@ -1046,21 +1062,16 @@ def main():
     else:
         rec["cpu_baseline"] = None
     rec.update(leg_res)
+    code = 0
     if world > 1:
         rec["roofline"]["launch_ms_rank0"] = round(ev_ms / args.steps, 4)
-        rec["ranks"] = ranks
-        rec["distinct_gpus"] = len({r["pci_bus_id"] for r in ranks})
-        rec["gather"] = rccl_gather(E, dist, rank, world, out, R, digests, rec) \
-            if do_gather else None
-        rec["rccl_ranks"] = rec["gather"].get("rccl_ranks") if rec["gather"] else None
+        gather = rccl_gather(E, dist, rank, world, out, R, digests, rec) if do_gather else None
+        code = multi_rank_fields(rec, ranks, gather, world, args.share_device)
     print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()
-    # a failed or unverified RCCL gather, or ranks that did not land on distinct
-    # GPUs, must not pass silently: the line above says what, the exit code too
-    if world > 1 and ((rec["gather"] or {}).get("error") or
-                      (not args.share_device and rec["distinct_gpus"] != world)):
-        sys.exit(4)
+    if code:
+        sys.exit(code)
 
 
 if __name__ == "__main__":
