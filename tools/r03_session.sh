@@ -27,7 +27,15 @@ while [ $# -gt 0 ]; do
     varprof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/varprof" -o k -- python3 "$ROOT/tools/varpath_crossover.py" --reps 10 > "$OUT/varprof.log" 2>&1) || { tail -20 "$OUT/varprof.log"; exit 1; }
              C="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
              (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/varpmc" -o k -- python3 "$ROOT/tools/varpath_crossover.py" --reps 3 > "$OUT/varpmc.log" 2>&1) || { tail -20 "$OUT/varpmc.log"; exit 1; }
-             python3 tools/pmc_summary.py "$OUT/varpmc" crc32c_chunk_kernel crc32c_finalize_kernel crc32c_direct_kernel plan_ sorted_ | tee "$OUT/varpmc.out" ;;
+             python3 tools/pmc_summary.py "$OUT/varpmc" crc32c_chunk_kernel crc32c_finalize_kernel crc32c_direct_kernel plan_ sorted_ | tee "$OUT/varpmc.out"
+             find "$OUT/varprof" -name '*kernel_stats.csv' -exec cp {} "$OUT/varprof_kernel_stats.csv" \;
+             rm -rf "$OUT/varprof" "$OUT/varpmc" ;;
+    flushprof) (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/flushprof" -o k -- "$ROOT/tools/flush_probe" 100 > "$OUT/flushprof.log" 2>&1) || { tail -20 "$OUT/flushprof.log"; exit 1; }
+             cp "$OUT"/flushprof/*/k_kernel_stats.csv "$OUT/flushprof_kernel_stats.csv" 2>/dev/null || find "$OUT/flushprof" -name '*kernel_stats.csv' -exec cp {} "$OUT/flushprof_kernel_stats.csv" \;
+             C="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+             (cd /tmp && timeout -s KILL 200 rocprofv3 --pmc $C --output-format csv -d "$OUT/flushpmc" -o k -- "$ROOT/tools/flush_probe" 20 > "$OUT/flushpmc.log" 2>&1) || { tail -20 "$OUT/flushpmc.log"; exit 1; }
+             python3 tools/pmc_summary.py "$OUT/flushpmc" direct | tee "$OUT/flushpmc.out"
+             rm -rf "$OUT/flushprof" "$OUT/flushpmc" ;;
     rehearsal) run bench_n2_rehearsal 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --share-device --steps 5 --warmup 2 --no-cpu ;;
     dlog) run bench_dlog 400 python bench.py --config dlog --steps 30 ;;
