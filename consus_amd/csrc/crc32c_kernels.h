@@ -132,8 +132,11 @@ struct SortedWorkspace
     uint4* items;        // item_cap 16-B descriptors
     uint64_t item_cap;   // sorted_item_cap(count, total_bytes)
 };
-// batches of at least this many bytes (the total known) take the sorted path
-constexpr uint64_t kSortedMinBytes = 64ull << 20;
+// batches of at least this many bytes (the total known) take the sorted path:
+// below it the piece path is 15-60 % faster, from it on the two are within
+// +-4 % up to ~2 GiB and the sorted path wins at configs[2]'s 4.9 GB
+// (tools/varpath_crossover.py, profiles/r03_varpath_crossover.txt)
+constexpr uint64_t kSortedMinBytes = 512ull << 20;
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);
 uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes);

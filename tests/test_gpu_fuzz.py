@@ -75,7 +75,7 @@ def test_fuzz_round(engine, oracle, round_):
         engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini, total_bytes=hint)
         assert np.array_equal(d_out.download(np.uint32, count), want), ("device", hint)
 
-    # the sorted path (forced here; the engine takes it by itself from 64 MiB),
+    # the sorted path (forced here; the engine takes it by itself from 512 MiB),
     # one workgroup per CU or a few workgroups (shares cut inside records)
     grid = [None, "1", "2", "5", "64"][int(rng.integers(0, 5))]
     os.environ["MI_CRC32C_VARPATH"] = "sorted"

@@ -2,7 +2,7 @@
 one team per whole record, records binned by row count inside each
 workgroup's cost-balanced share, split records (> 64 KiB) XORed together
 from 64 KiB pieces.  Forced here with MI_CRC32C_VARPATH=sorted (the engine
-takes it by itself for batches of >= 64 MiB); every result is compared with
+takes it by itself for batches of >= 512 MiB); every result is compared with
 the CPU oracle, bit-exact, and the path is checked to have run
 (mi_crc32c_stats().sorted_batches).
 """
@@ -257,16 +257,22 @@ def test_sorted_matches_piece_path(engine, oracle):
 
 
 def test_sorted_default_for_large_batches(engine, oracle):
-    """Without the knob, a batch of >= 64 MiB takes the sorted path."""
+    """Without the knob, a batch of >= 512 MiB takes the sorted path and one
+    just below it the piece path (kSortedMinBytes, the measured crossover)."""
     rng = np.random.default_rng(19)
-    count = 20_000
-    lengths = rng.integers(3000, 4000, count).astype(np.uint32)
+    count = 160_000
+    lengths = rng.integers(3300, 3500, count).astype(np.uint32)
+    assert int(lengths.sum(dtype=np.uint64)) >= 512 << 20
     offsets, end = _packed(rng, lengths)
     buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    want = oracle.batch(buf, offsets, lengths)
     before = engine.stats()["sorted_batches"]
-    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
-                          oracle.batch(buf, offsets, lengths))
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths), want)
     assert engine.stats()["sorted_batches"] == before + 1
+    k = int(np.searchsorted(np.cumsum(lengths, dtype=np.uint64), np.uint64(512 << 20)))
+    before = engine.stats()["sorted_batches"]
+    assert np.array_equal(_device_run(engine, buf, offsets[:k], lengths[:k]), want[:k])
+    assert engine.stats()["sorted_batches"] == before
 
 
 @pytest.mark.parametrize("seed", range(10))
