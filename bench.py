@@ -387,7 +387,7 @@ def cpu_baseline(args) -> dict:
             "first_crc": int(crc_ref[0])}
 
 
-def run_dlog(args) -> dict:
+def run_dlog(args, compact: bool = False) -> dict:
     """The batching durable log driven as txman drives it (tools/dlog_bench.cc):
     8 threads append 400K entries each (42-1024 B), the caller waits for the
     watermark to cover them, then the log is replayed (GPU-verified scan of
@@ -451,6 +451,10 @@ def run_dlog(args) -> dict:
     ceiling = {"appends_per_s": round(nc["appends_per_s"], 1), "per_flush": per_flush(nc),
                "note": "same front-end with a no-op flush checksum: the appenders' own limit",
                "runs": [round(x["appends_per_s"], 1) for x in runs["no-checksum"]]}
+    if compact:  # a leg of the default line: the per-run detail stays out
+        ceiling.pop("per_flush")
+        if cpu:
+            cpu["runs"] = [round(x["appends_per_s"], 1) for x in cpu["runs"]]
     return {"metric": "durable-log appends/s, 8 appending threads, GPU batch CRC per flushed "
                       "segment (txman/durable_log.cc append contract)",
             "value": round(best["appends_per_s"], 1), "unit": "appends/s", "n_gpus": 1,
@@ -458,7 +462,10 @@ def run_dlog(args) -> dict:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: entry lengths uniform 42-1024 B, splitmix64 bytes",
             "config": {"workload": f"{threads} threads x {per} appends, then wait for the "
-                                   f"watermark; segment files on tmpfs", "runs": runs["gpu"]},
+                                   f"watermark; segment files on tmpfs",
+                       "runs": [round(x["appends_per_s"], 1) for x in runs["gpu"]] if compact
+                       else runs["gpu"]},
+            "durable_latency_us": best["durable_latency_us"],
             "flush": pf, "frontend_ceiling": ceiling,
             "roofline": None, "cpu_baseline": cpu,
             "digest_verified": all(x["replayed"] == x["appends"] and x["replay_bad"] == 0
@@ -887,6 +894,9 @@ def main():
             # preparation with the GPU idle, and 5 steps leave it in the clock ramp
             sub = sub_args(args, cfg, **({"warmup": max(args.warmup, 100)} if cfg == "zipf" else {}))
             legs.append((key, sub, pmc_traffic(sub) if not args.no_pmc else (None, "skipped")))
+        # the durable-log front-end: appends/s and the per-flush
+        # GPU batch against its bound, beside the reference CPU checksum
+        legs.append(("durable_log", sub_args(args, "dlog", steps=30), (None, "n/a")))
 
     if args.config == "dlog":  # a child process drives the engine; none here
         if rank == 0:
@@ -1018,7 +1028,7 @@ def main():
     for key, sub, tr in legs:
         t_leg = time.perf_counter()
         try:
-            r = run_secondary(sub, E, tr)
+            r = run_dlog(sub, compact=True) if sub.config == "dlog" else run_secondary(sub, E, tr)
             for k in ("n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
                 r.pop(k, None)
         except Exception as e:  # noqa: BLE001 -- a leg must not lose the headline line

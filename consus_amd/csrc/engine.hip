@@ -284,7 +284,12 @@ struct PinBuf
     {
         if (bytes <= cap) return MI_CRC32C_OK;
         release();
-        size_t want = std::max<size_t>(bytes, 4096);
+        // powers of two from 64 KiB: pinning costs milliseconds, and a
+        // durable log's flushes grow a few percent at a time (each regrowth
+        // was a multi-ms stall of the flush thread: the p99 durability
+        // latency of round 3's first dlog runs)
+        size_t want = size_t(64) << 10;
+        while (want < bytes) want <<= 1;
         if (hipHostMalloc(&p, want, hipHostMallocMapped) != hipSuccess)
         {
             p = nullptr;
