@@ -108,6 +108,7 @@ class __attribute__((visibility("default"))) durable_log
             uint64_t frames;
         };
         void flush();
+        void warm_up();
         void writer();
         void sync();
         int64_t append_slow(segment* seg);
