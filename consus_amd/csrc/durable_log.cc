@@ -370,6 +370,7 @@ durable_log::durable_log(const durable_log_options& options)
     , m_ext_peak(0)
 {
     for (auto& t : m_flush_ns) t.store(0);
+    for (auto& t : m_flush_max_ns) t.store(0);
     m_flush = std::thread(&durable_log::flush, this);
     m_writer = std::thread(&durable_log::writer, this);
     m_sync = std::thread(&durable_log::sync, this);
@@ -431,6 +432,20 @@ uint64_t durable_log::frames_flushed() const { return m_frames_flushed; }
 void durable_log::flush_seconds(double out[6]) const
 {
     for (int i = 0; i < 6; ++i) out[i] = double(m_flush_ns[i].load()) * 1e-9;
+}
+
+void durable_log::flush_max_seconds(double out[6]) const
+{
+    for (int i = 0; i < 6; ++i) out[i] = double(m_flush_max_ns[i].load()) * 1e-9;
+}
+
+void durable_log::note_phase(int phase, uint64_t ns)
+{
+    m_flush_ns[phase] += ns;
+    uint64_t m = m_flush_max_ns[phase].load(std::memory_order_relaxed);
+    while (ns > m && !m_flush_max_ns[phase].compare_exchange_weak(m, ns, std::memory_order_relaxed))
+    {
+    }
 }
 
 void durable_log::set_fsync_delay_for_testing(uint32_t microseconds)
@@ -804,7 +819,7 @@ int durable_log::prepare_segment(segment* seg, uint64_t& n, uint64_t& used, writ
     auto t = std::chrono::steady_clock::now();
     auto lap = [&](int phase) {
         const auto u = std::chrono::steady_clock::now();
-        m_flush_ns[phase] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(u - t).count());
+        note_phase(phase, uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(u - t).count()));
         t = u;
     };
     job->log = this;
@@ -898,9 +913,9 @@ int durable_log::write_out(write_job* job)
         !pwrite_all(job->fd, job->arena + at, job->used - at, off_t(file)))
         return errno;
     job->release_ext();
-    m_flush_ns[4] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+    note_phase(4, uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                   std::chrono::steady_clock::now() - t)
-                                  .count());
+                                  .count()));
     return 0;
 }
 
@@ -959,9 +974,9 @@ void durable_log::sync()
         const auto t = std::chrono::steady_clock::now();
         int e = fsync(job.fd) < 0 ? errno : 0;
         if (const uint32_t us = m_fsync_delay_us.load()) usleep(us);
-        m_flush_ns[5] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+        note_phase(5, uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                       std::chrono::steady_clock::now() - t)
-                                      .count());
+                                      .count()));
         hold.lock();
         m_pending.erase(m_pending.begin());
         if (e)
@@ -1073,9 +1088,9 @@ void durable_log::flush()
             else
                 usleep(20);
         }
-        m_flush_ns[0] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+        note_phase(0, uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                       std::chrono::steady_clock::now() - t_wait)
-                                      .count());
+                                      .count()));
         if (!exact)
         {
             // the segment filled up: the valid frames end at the first
@@ -1223,6 +1238,7 @@ uint64_t mi_dlog_flushes(mi_dlog* l) { return l->log.flushes(); }
 uint64_t mi_dlog_frames_flushed(mi_dlog* l) { return l->log.frames_flushed(); }
 uint64_t mi_dlog_external_peak(mi_dlog* l) { return l->log.external_bytes_peak(); }
 void mi_dlog_flush_seconds(mi_dlog* l, double out[6]) { l->log.flush_seconds(out); }
+void mi_dlog_flush_max_seconds(mi_dlog* l, double out[6]) { l->log.flush_max_seconds(out); }
 void mi_dlog_set_batch_crc_for_testing(mi_dlog* l, mi_dlog_batch_crc fn, void* ctx)
 {
     l->log.set_batch_crc_for_testing(fn, ctx);

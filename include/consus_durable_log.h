@@ -45,6 +45,8 @@ uint64_t mi_dlog_external_peak(mi_dlog* log);
  * [2] the batch CRC (GPU), [3] writing the CRCs into the frames, [4] pwrite,
  * [5] fsync.  For tuning; any of out[0..5] may be read at any time. */
 void mi_dlog_flush_seconds(mi_dlog* log, double out[6]);
+/* The longest single occurrence of each of those phases, seconds. */
+void mi_dlog_flush_max_seconds(mi_dlog* log, double out[6]);
 
 /* Test hook (call before open): batch CRC engine other than the GPU. */
 typedef int (*mi_dlog_batch_crc)(void* ctx, const void* base, const uint64_t* offsets,

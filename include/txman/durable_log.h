@@ -92,6 +92,8 @@ class __attribute__((visibility("default"))) durable_log
         // Seconds spent per phase: copy wait, frame walk, batch CRC, CRC
         // patch, pwrite (flush thread), fsync (sync thread).
         void flush_seconds(double out[6]) const;
+        // the longest single occurrence of each phase (same order), seconds
+        void flush_max_seconds(double out[6]) const;
         // Test hook: every fsync also sleeps this long (a slow disk on tmpfs).
         void set_fsync_delay_for_testing(uint32_t microseconds);
         // Most bytes of oversized frames (staged outside the arenas) held at
@@ -146,6 +148,8 @@ class __attribute__((visibility("default"))) durable_log
         std::atomic<uint64_t> m_flushes;
         std::atomic<uint64_t> m_frames_flushed;
         std::atomic<uint64_t> m_flush_ns[6];
+        std::atomic<uint64_t> m_flush_max_ns[6];
+        void note_phase(int phase, uint64_t ns);
         std::vector<uint64_t> m_offs;   // flush thread: the sealed segment's frames
         std::vector<uint32_t> m_lens;
         std::vector<uint32_t> m_crcs;

@@ -220,6 +220,7 @@ int main(int argc, char** argv)
     log.wake();
     monitor.join();
     std::vector<double> lat;
+    double worst = -1, worst_at = 0;  // the longest wait and when (s after the start) it began
     for (const auto& v : samples)
         for (const auto& [r, ta] : v)
         {
@@ -228,14 +229,19 @@ int main(int argc, char** argv)
                                        [](int64_t rr, const std::pair<double, int64_t>& m) {
                                            return rr < m.second;
                                        });
-            if (it != marks.end()) lat.push_back(std::max(0.0, it->first - ta) * 1e6);
+            if (it != marks.end())
+            {
+                lat.push_back(std::max(0.0, it->first - ta) * 1e6);
+                if (lat.back() > worst) worst = lat.back(), worst_at = ta - t0;
+            }
         }
     std::sort(lat.begin(), lat.end());
     auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[size_t(q * (lat.size() - 1))]; };
     const uint64_t flushes = log.flushes(), frames = log.frames_flushed();
     const int err = log.error();
-    double fs[6];
+    double fs[6], fm[6];
     log.flush_seconds(fs);
+    log.flush_max_seconds(fm);
 
     // the replay: every record back, in order, byte-exact
     Replay rp{&rec_len, &rec_at, pool.data()};
@@ -256,8 +262,10 @@ int main(int argc, char** argv)
            "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
            "\"flush_s\": {\"copy_wait\": %.4f, \"walk\": %.4f, \"batch_crc\": %.4f, "
            "\"patch\": %.4f, \"pwrite\": %.4f, \"fsync\": %.4f}, "
+           "\"flush_max_us\": {\"copy_wait\": %.1f, \"walk\": %.1f, \"batch_crc\": %.1f, "
+           "\"patch\": %.1f, \"pwrite\": %.1f, \"fsync\": %.1f}, "
            "\"durable_latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, "
-           "\"samples\": %zu}}\n",
+           "\"max_at_s\": %.4f, \"samples\": %zu}}\n",
            fake ? "none" : g_ref ? "reference-cpu" : "gpu", empty_us, threads,
            (unsigned long long)total,
            (unsigned long long)entry_bytes,
@@ -265,7 +273,8 @@ int main(int argc, char** argv)
            double(total) / (t_durable - t0), double(frame_bytes) / (t_durable - t0) / (1u << 30),
            (unsigned long long)flushes, (unsigned long long)frames,
            (unsigned long long)failures.load(), err, (long long)n, (unsigned long long)rp.bad,
-           fs[0], fs[1], fs[2], fs[3], fs[4], fs[5], pct(0.5), pct(0.99),
-           lat.empty() ? 0.0 : lat.back(), lat.size());
+           fs[0], fs[1], fs[2], fs[3], fs[4], fs[5], fm[0] * 1e6, fm[1] * 1e6, fm[2] * 1e6,
+           fm[3] * 1e6, fm[4] * 1e6, fm[5] * 1e6, pct(0.5), pct(0.99),
+           lat.empty() ? 0.0 : lat.back(), worst_at, lat.size());
     return (failures.load() || err || n != int64_t(total) || rp.bad) ? 1 : 0;
 }
