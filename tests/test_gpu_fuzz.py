@@ -2,8 +2,9 @@
 variable-length entry point: host batches on the direct kernel and on the
 planned path, device batches with and without the size hint, fixed-stride
 batches (also split over 2-5 ranges through the multi-device entry
-points), the sorted path at random grids, the opt-in stream path, and
-single buffers (host and device).  Shapes mix empty, tiny,
+points), the sorted path at random grids, the direct kernel's two forms
+and its zero-copy read from pinned memory, and single buffers (host and
+device).  Shapes mix empty, tiny,
 row- and chunk-edge, and multi-chunk records; offsets packed, random,
 overlapping and unordered; inits random or absent.
 
@@ -55,6 +56,23 @@ def test_fuzz_round(engine, oracle, round_):
     for planned in (False, True):
         got = engine.crc32c_batch(buf, offsets, lengths, inits, planned=planned)
         assert np.array_equal(got, want), ("host", planned)
+    # the direct kernel's LDS image and LDS-free forms, and the same bytes read
+    # in place from mapped pinned memory (the durable log's flush path)
+    if int(lengths.max()) <= 16384:
+        try:
+            for lite in ("0", "1"):
+                os.environ["MI_CRC32C_DIRECT_LITE"] = lite
+                got = engine.crc32c_batch(buf, offsets, lengths, inits)
+                assert np.array_equal(got, want), ("direct", lite)
+        finally:
+            os.environ.pop("MI_CRC32C_DIRECT_LITE", None)
+        pinned = engine.PinnedBuffer(size)
+        try:
+            pinned.array[:] = buf
+            got = engine.crc32c_batch(pinned.array, offsets, lengths, inits)
+            assert np.array_equal(got, want), "zero-copy"
+        finally:
+            pinned.free()
     # the multi-device entry point, split into 2-5 byte-balanced ranges on the one GPU
     ndev = int(rng.integers(2, 6))
     got = engine.crc32c_batch_multi(buf, offsets, lengths, inits, devices=[0] * ndev, shard_min=1)
