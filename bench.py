@@ -52,6 +52,14 @@ import time
 
 import numpy as np
 
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One line per stage on stderr (stdout carries only the JSON line): a
+    long default run shows where it is."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -883,6 +891,7 @@ def main():
     traffic, traffic_note = (None, "skipped")
     if rank == 0 and world == 1 and not args.child_pmc and not args.no_pmc and \
             args.config in ("fixed4k", "zipf", "single", "stream", "pcie4k"):
+        progress(f"PMC traffic pass ({args.config})")
         traffic, traffic_note = pmc_traffic(args)
     # The other single-GPU BASELINE configs ride in the headline line (N = 1):
     # configs[2], configs[4] and configs[1]'s bytes starting in host memory.
@@ -893,6 +902,7 @@ def main():
             # the zipf leg warms up for >= 100 steps (~80 ms): it starts after host-side
             # preparation with the GPU idle, and 5 steps leave it in the clock ramp
             sub = sub_args(args, cfg, **({"warmup": max(args.warmup, 100)} if cfg == "zipf" else {}))
+            progress(f"PMC traffic pass ({cfg})")
             legs.append((key, sub, pmc_traffic(sub) if not args.no_pmc else (None, "skipped")))
         # the durable-log front-end: appends/s and the per-flush
         # GPU batch against its bound, beside the reference CPU checksum
@@ -905,6 +915,7 @@ def main():
 
     # The engine is loaded before torch so both bind the /opt/rocm HIP runtime.
     import consus_amd as E
+    progress("engine init")
     E.init(0 if args.share_device else local)
     if args.config != "fixed4k" and not (args.config in ("single", "zipf") and world > 1):
         if world != 1:
@@ -1005,6 +1016,7 @@ def main():
     # few seconds (the per-launch rate must not droop with clocks or power;
     # it also keeps the GPU busy long enough for a utilisation sampler).
     sustained = None
+    progress("timed steps done; sustained leg")
     if args.sustain_seconds > 0:
         E.sync()
         E.timer_start()
@@ -1028,6 +1040,7 @@ def main():
     for key, sub, tr in legs:
         t_leg = time.perf_counter()
         try:
+            progress(f"leg {key}")
             r = run_dlog(sub, compact=True) if sub.config == "dlog" else run_secondary(sub, E, tr)
             for k in ("n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
                 r.pop(k, None)
@@ -1076,6 +1089,7 @@ def main():
         "sustained": sustained,
     }
     if world == 1 and not args.no_cpu:
+        progress("CPU baseline")
         rec["cpu_baseline"] = cpu_baseline(args)
     else:
         rec["cpu_baseline"] = None
