@@ -6,7 +6,7 @@
 # script stops at the first failure.  Output: gpurun_out/prof_<TAG>/.
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-TAG="${1:-r02}"
+TAG="${1:-r03}"
 OUT="$ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -19,7 +19,7 @@ run() {  # name limit cmd...
 stats() {  # config extra-args...
   local c=$1; shift
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_$c" -o k --output-format csv \
-     -- python3 "$ROOT/bench.py" --config "$c" --no-cpu --no-pmc --sustain-seconds 0 --steps 30 --warmup 300 "$@" > "$OUT/rocprof_$c.log" 2>&1) \
+     -- python3 "$ROOT/bench.py" --config "$c" --no-cpu --no-pmc --no-legs --sustain-seconds 0 --steps 30 --warmup 300 "$@" > "$OUT/rocprof_$c.log" 2>&1) \
      || { echo "FAILED rocprof $c"; tail -20 "$OUT/rocprof_$c.log"; exit 1; }
   cp "$(find "$OUT/rocprof_$c" -name '*kernel_stats.csv' | head -1)" "$OUT/${c}_kernel_stats.csv"
 }
