@@ -421,6 +421,7 @@ def run_dlog(args, compact: bool = False) -> dict:
             for name, extra in engines:
                 env = dict(os.environ)
                 env.update(extra)
+                progress(f"durable log run: {name}")
                 r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(per), "42", "1024"],
                                    capture_output=True, text=True, timeout=300, env=env)
                 if r.returncode != 0:

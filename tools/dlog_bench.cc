@@ -25,6 +25,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 #include <string>
@@ -154,6 +156,40 @@ int main(int argc, char** argv)
         }
     }
     consus::durable_log log(seg);
+    // watchdog: a stage that takes more than DLOG_STAGE_LIMIT s (default 60)
+    // prints where the run is and the log's counters, then ends the process
+    std::atomic<int> stage{0};
+    static const char* const kStage[] = {"open", "append", "durable", "monitor", "replay", "close",
+                                         "done"};
+    std::atomic<bool> wd_stop{false};
+    const double wd_limit = getenv("DLOG_STAGE_LIMIT") ? atof(getenv("DLOG_STAGE_LIMIT")) : 60.0;
+    std::thread watchdog([&] {
+        int last = -1;
+        double since = now();
+        while (!wd_stop.load())
+        {
+            usleep(100000);
+            const int st = stage.load();
+            if (st != last) last = st, since = now();
+            if (now() - since > wd_limit)
+            {
+                double f[6], m[6];
+                log.flush_seconds(f);
+                log.flush_max_seconds(m);
+                fprintf(stderr,
+                        "dlog_bench: stage '%s' exceeded %.0f s: durable %lld, flushes %llu, frames "
+                        "flushed %llu, error %d; flush s: wait %.3f walk %.3f crc %.3f patch %.3f "
+                        "pwrite %.3f fsync %.3f; max us: %.0f %.0f %.0f %.0f %.0f %.0f\n",
+                        kStage[st], wd_limit, (long long)log.durable(),
+                        (unsigned long long)log.flushes(),
+                        (unsigned long long)log.frames_flushed(), log.error(), f[0], f[1], f[2],
+                        f[3], f[4], f[5], m[0] * 1e6, m[1] * 1e6, m[2] * 1e6, m[3] * 1e6,
+                        m[4] * 1e6, m[5] * 1e6);
+                fflush(stderr);
+                _exit(3);
+            }
+        }
+    });
     if (g_ref) log.set_batch_crc_for_testing(ref_batch, nullptr);
     if (fake)
         log.set_batch_crc_for_testing(
@@ -210,15 +246,19 @@ int main(int argc, char** argv)
     });
     while (ready.load() < threads) std::this_thread::yield();
     const double t0 = now();
+    stage.store(1);
     go.store(true, std::memory_order_release);
     for (auto& th : ths) th.join();
     const double t_appended = now();
+    stage.store(2);
     int64_t x = log.durable();
     while (x <= int64_t(total) && !log.error()) x = log.wait(x);
     const double t_durable = now();
+    stage.store(3);
     stop.store(true);
     log.wake();
     monitor.join();
+    stage.store(4);
     std::vector<double> lat;
     double worst = -1, worst_at = 0;  // the longest wait and when (s after the start) it began
     for (const auto& v : samples)
@@ -254,7 +294,11 @@ int main(int argc, char** argv)
                 ++r->bad;
         },
         &rp);
+    stage.store(5);
     log.close();
+    stage.store(6);
+    wd_stop.store(true);
+    watchdog.join();
     const uint64_t frame_bytes = entry_bytes + total * 20;
     printf("{\"engine\": \"%s\", \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
            "\"append_s\": %.6f, \"durable_s\": %.6f, \"appends_per_s\": %.1f, "
