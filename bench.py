@@ -417,7 +417,10 @@ def run_dlog(args, compact: bool = False) -> dict:
     engines.append(("no-checksum", {"FAKE_CRC": "1"}))
     runs = {name: [] for name, _ in engines}
     try:
-        for _ in range(max(1, args.steps // 10)):
+        # 5 runs per engine at the default 30 steps: a run's rate swings 1.5x with
+        # how the appenders, the flush thread and the writer share the host's
+        # cores, so the line reports the median of five
+        for _ in range(max(1, args.steps // 6)):
             for name, extra in engines:
                 env = dict(os.environ)
                 env.update(extra)

@@ -88,9 +88,10 @@ constexpr uint64_t kDirectMaxBytes = 32ull << 20;  // sum of lengths
 constexpr uint64_t kDirectMaxRecord = 16u << 10;   // longest record (128 rows for one team;
                                                    // the planned path wins above ~32 KiB)
 // Batches of at most kLiteMaxBytes (a durable-log flush) take the LDS-free
-// form: 256-thread workgroups, no 152 KiB table staging.
+// form: one-wave workgroups, no 152 KiB table staging.
 constexpr uint64_t kLiteMaxBytes = 2ull << 20;
-constexpr int kLiteBlock = 256;
+constexpr int kLiteBlock = 256;   // launch bound of the LDS-free form
+constexpr uint32_t kLiteWG = 64;  // ... and the workgroup it is launched with
 // Completion word: when `signal` is set, the last workgroup to finish stores
 // `seq` to signal->flag (mapped host memory) after every CRC is visible
 // system-wide, so the host may spin on it instead of a stream sync.

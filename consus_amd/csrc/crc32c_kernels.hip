@@ -1358,7 +1358,7 @@ hipError_t launch_var_finalize(const void* base, const uint64_t* offsets, const 
 // by the row update and team fold of the fixed kernel, and finished with the
 // seed: crc = ~(Z_L(~init) ^ raw).  Rows go 8 at a time (one load group).
 // ---------------------------------------------------------------------------
-// LITE (batches up to kLiteMaxBytes): 256-thread workgroups, no LDS; the
+// LITE (batches up to kLiteMaxBytes): one-wave workgroups (launch bound 256), no LDS; the
 // row update and the fold go through the lane tables (row_update_lane,
 // team_fold_lane), 42 VGPRs loaded from L2 beside the first record's reads,
 // instead of a 152 KiB LDS image staged by every workgroup before any
@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(LITE ? kLiteBlock : kBlock, 1) void crc32c_direct_k
     uint32_t* __restrict__ out, const uint32_t* __restrict__ tables,
     const uint32_t* __restrict__ pow2, DoneSignal sig)
 {
-    constexpr int B = LITE ? kLiteBlock : kBlock;
+    const uint32_t B = LITE ? blockDim.x : uint32_t(kBlock);
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t li = lane_info();
     const uint64_t team = (uint64_t(blockIdx.x) * B + threadIdx.x) / kTeam;
@@ -1516,10 +1516,15 @@ hipError_t launch_direct(const void* base, const uint64_t* offsets, const uint32
     if (lite < 0) lite = total_bytes <= kLiteMaxBytes;
     if (lite)
     {
-        // 32 teams per workgroup; up to 4 workgroups per CU
-        const uint64_t need = (count + (kLiteBlock / kTeam) - 1) / (kLiteBlock / kTeam);
-        const uint64_t g = std::min<uint64_t>(need, uint64_t(grid) * 4);
-        hipLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(uint32_t(g)), dim3(kLiteBlock), 0, stream,
+        // one-wave workgroups (8 teams): a flush's records spread over as many
+        // CUs as it has waves, so more of its PCIe reads are in flight at once
+        // (round 3 A/B, tools/wg_ab.sh, profiles/r03_lite_wg_ab.txt: a 270-frame
+        // zero-copy flush 17.3-18.7 us against 18.9-19.8 with 256-thread
+        // workgroups, never slower up to 8,192 frames); up to 16 per CU
+        constexpr uint32_t wg = kLiteWG;
+        const uint64_t need = (count + (wg / kTeam) - 1) / (wg / kTeam);
+        const uint64_t g = std::min<uint64_t>(need, uint64_t(grid) * (4 * kLiteBlock / wg));
+        hipLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(uint32_t(g)), dim3(wg), 0, stream,
                            static_cast<const uint8_t*>(base), offsets, lengths, inits, count, out,
                            tables, pow2, sig);
         return hipGetLastError();
