@@ -1518,7 +1518,7 @@ hipError_t launch_direct(const void* base, const uint64_t* offsets, const uint32
     {
         // one-wave workgroups (8 teams): a flush's records spread over as many
         // CUs as it has waves, so more of its PCIe reads are in flight at once
-        // (round 3 A/B, tools/wg_ab.sh, profiles/r03_lite_wg_ab.txt: a 270-frame
+        // (round 3 A/B, profiles/r03_lite_wg_ab.txt: a 270-frame
         // zero-copy flush 17.3-18.7 us against 18.9-19.8 with 256-thread
         // workgroups, never slower up to 8,192 frames); up to 16 per CU
         constexpr uint32_t wg = kLiteWG;
