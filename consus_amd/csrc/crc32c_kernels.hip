@@ -2482,17 +2482,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint4 b[RB];
 #pragma unroll
     for (int j = 0; j < RB - 1; ++j) b[j] = load16(row_ptr(cur0, j, false));
+    if (RB == 2 && shA.n == 2) b[1] = load16(row_ptr(cur0, 1, false));
     __builtin_amdgcn_sched_barrier(0);
     // One group: hash `cur` (shape sh) while the next group's view is built
     // into `nxt`.  The loop runs it twice per iteration with the two views
     // swapped (round 2 A/B: profiles/r02_sorted_view32_pingpong_ab.txt), so the ~20 registers of a view are never
     // copied at the back edge.
     auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
-        // A 2-row group runs no body loop, so its last row can be issued now,
-        // a whole group header ahead of its folding, instead of one row
-        // ahead (round 2 A/B: profiles/r02_sorted_shortpre_ab.txt); b[1] is free here.
+        // A 2-row group runs no body loop: its row 1 was issued at the end of
+        // the previous step, into b[1] once that step's last row was folded
+        // (see below), a whole fold, finish and group header ahead.
         const bool pre = RB == 2 && sh.n == 2;
-        if (pre) b[1] = load16(row_ptr(cur, 1, false));
         const uint32_t g_nn = grab();
         const uint4 d_nn = load_desc(g_nn);
         shn = shape_of(d_nxt, g_nxt);
@@ -2564,6 +2564,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             __builtin_amdgcn_sched_barrier(0);
             gen_row(b[j], n - RB + j);
         }
+        // the next group's row 1 if it has two rows (b[1] is free now)
+        if (RB == 2 && shn.n == 2) b[1] = load16(row_ptr(nxt, 1, false));
         const uint32_t W = team_fold(V);
         flush();  // the previous group's items
         {
