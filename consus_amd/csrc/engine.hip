@@ -50,6 +50,12 @@ constexpr uint64_t kZeroCopyMax = uint64_t(8) << 10;  // packed inputs read in p
 // long the host spins on it before it blocks in a stream sync
 constexpr int kDoneWord = 16;
 constexpr int kDoneSpinUs = 1000;
+// ... and up to which batch size (bytes hashed) it beats the stream sync:
+// above ~2 MB the sync returned 5-14 us sooner (tools/flush_probe, 3 rounds:
+// 4,096 frames / 2.28 MB 78.7-83.2 us vs 84.3-88.0; 8,192 / 4.56 MB
+// 138.5-146.0 vs 152.4-159.7; 2,048 / 1.13 MB still 1-2 us slower;
+// profiles/r03_done_word_crossover.txt)
+constexpr uint64_t kDoneWordMaxBytes = uint64_t(2) << 20;
 
 // MI_CRC32C_DONE_WORD=0: synchronous direct launches wait in a stream sync
 // instead of spinning on their completion word (A/B; read per batch).
@@ -347,11 +353,13 @@ struct Ctx
         HIP_TRY(hipMemset(done_ctr.p, 0, 64));
         return pin_small.reserve(4096);
     }
-    // The completion word of the next synchronous direct launch (nullptr: the
-    // pinned page has no device mapping; then the caller syncs the stream).
-    bool next_signal(DoneSignal* s)
+    // The completion word of the next synchronous direct launch of `bytes`
+    // (false: the pinned page has no device mapping, or the batch is larger
+    // than kDoneWordMaxBytes; then the caller syncs the stream).
+    bool next_signal(DoneSignal* s, uint64_t bytes)
     {
-        if (!pin_small.dev || !done_ctr.p || done_word_disabled()) return false;
+        if (!pin_small.dev || !done_ctr.p || bytes > kDoneWordMaxBytes || done_word_disabled())
+            return false;
         volatile uint32_t* h = pin_small.as<uint32_t>() + kDoneWord;
         *h = 0;
         if (++done_seq == 0) done_seq = 1;
@@ -796,7 +804,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
                 if (inits) std::memcpy(hp + count * 12, inits, count * 4);
                 const uint8_t* sp = static_cast<const uint8_t*>(c->pin_stage.dev);
                 DoneSignal sig;
-                const bool signalled = c->next_signal(&sig);
+                const bool signalled = c->next_signal(&sig, total);
                 HIP_TRY(launch_direct(zsrc, reinterpret_cast<const uint64_t*>(sp),
                                       reinterpret_cast<const uint32_t*>(sp + count * 8),
                                       inits ? reinterpret_cast<const uint32_t*>(sp + count * 12)
@@ -845,7 +853,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         {
             const uint8_t* sp = static_cast<const uint8_t*>(c->pin_stage.dev);
             DoneSignal sig;
-            const bool signalled = c->next_signal(&sig);
+            const bool signalled = c->next_signal(&sig, total);
             HIP_TRY(launch_direct(sp + data_at, reinterpret_cast<const uint64_t*>(sp),
                                   reinterpret_cast<const uint32_t*>(sp + count * 8),
                                   inits ? reinterpret_cast<const uint32_t*>(sp + count * 12)
