@@ -2155,8 +2155,8 @@ __device__ __forceinline__ uint32_t init_dword(uint32_t ninit, int32_t q, int k)
     return (dd > -4 && dd < 4) ? x : 0u;
 }
 
-// The masks depend on the record's init, loaded here and consumed a group
-// later (sort_view runs for the NEXT group), so the load costs no wait.
+// The masks depend on the record's init, loaded here (when there is an init
+// array) and consumed a group later (sort_view runs for the NEXT group).
 // 32-bit window arithmetic (an item spans < 2^17 bytes); one 64-bit add for
 // the row pointer.  The init word: (hi:lo) = ~init << 8 (q & 3) goes to
 // dwords q>>2 and q>>2 + 1 of the lane's block (q = the record's first byte
@@ -2164,7 +2164,6 @@ __device__ __forceinline__ uint32_t init_dword(uint32_t ninit, int32_t q, int k)
 // shifts per view: SQ_INSTS_VALU -9 % on the < 256 B class.)
 __device__ __forceinline__ SortView sort_view(const uint4& d, int32_t n, uint32_t tl,
                                               const uint32_t* __restrict__ inits,
-                                              const uint32_t* __restrict__ zero_word,
                                               const uint32_t* __restrict__ ones_word)
 {
     SortView v;
@@ -2185,8 +2184,13 @@ __device__ __forceinline__ SortView sort_view(const uint4& d, int32_t n, uint32_
     v.kf = make_uint4(keep_from(bs, 0), keep_from(bs, 1), keep_from(bs, 2), keep_from(bs, 3));
     v.ke = make_uint4(keep_below(ce, 0), keep_below(ce, 1), keep_below(ce, 2), keep_below(ce, 3));
     const bool with_init = L && (!(d.w & kSortMulti) || (d.w & kSortFirst));
-    // always one load (0 without inits, all ones where no init word goes in)
-    const uint32_t ninit = ~*(!with_init ? ones_word : inits ? inits + (d.w & kSortRecMask) : zero_word);
+    // With an init array: one load per lane (all ones, i.e. ~init = 0, where
+    // no init word goes in).  Without one (a uniform kernel argument): no load
+    // and no wait, ~init is all ones where the init word goes in, 0 elsewhere
+    // (round 3 A/B, profiles/r03_sorted_initskip_ab.txt: -1.5 to -2 us per
+    // configs[2] step).
+    const uint32_t ninit = inits ? ~*(!with_init ? ones_word : inits + (d.w & kSortRecMask))
+                                 : (with_init ? 0xFFFFFFFFu : 0u);
     const uint64_t sh = uint64_t(ninit) << ((uint32_t(q) & 3u) * 8u);
     const uint32_t xl = uint32_t(sh), xh = uint32_t(sh >> 32);
     const int32_t qd = q >> 2;  // arithmetic: -1 for q in -3..-1
@@ -2384,7 +2388,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint32_t tw = lane / kTeam;
     const uint32_t li = lane_info();
     const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
-    const uint32_t* zero_word = tables + kTabZero;
     const uint32_t* ones_word = tables + kTabFInit;  // Z_0(~0) = 0xFFFFFFFF
     const uint32_t* zneg = tables + kTabZNeg;
     // An item is finished one group late: right after its fold, lane q < 4 of
@@ -2467,7 +2470,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint32_t g_nxt = grab();
     uint4 d_nxt = load_desc(g_nxt);
     Shape shA = shape_of(d_cur, g_cur);
-    SortView vA = sort_view(d_cur, shA.n, tl, inits, zero_word, ones_word);
+    SortView vA = sort_view(d_cur, shA.n, tl, inits, ones_word);
     Shape shB{0, 0, 0, 0};
     SortView vB = vA;
     const SortView& cur0 = vA;
@@ -2496,7 +2499,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const uint32_t g_nn = grab();
         const uint4 d_nn = load_desc(g_nn);
         shn = shape_of(d_nxt, g_nxt);
-        nxt = sort_view(d_nxt, shn.n, tl, inits, zero_word, ones_word);
+        nxt = sort_view(d_nxt, shn.n, tl, inits, ones_word);
         uint32_t V[4] = {0, 0, 0, 0};
         const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
         // General row: padding skip, start mask and init word (rows up to
