@@ -119,6 +119,22 @@ __device__ __forceinline__ uint32_t zG(uint32_t base, uint32_t v)
            lds32(base + 3072 + ((v >> 22) & 0x3FCu));
 }
 
+// Z_n(v) for a per-lane n in 0..16 from the slice-by-16 tables: byte j of v
+// leaves the register after n - j zero bytes (T_{n-1-j}), bytes j >= n shift
+// down by n bytes.
+__device__ __forceinline__ uint32_t zT_n(uint32_t v, uint32_t n)
+{
+    uint32_t x = n >= 4 ? 0u : v >> (8 * n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+        const int32_t t = int32_t(n) - 1 - j;
+        const uint32_t e = lds32(kLdsT + uint32_t(max(t, 0)) * 1024u + ((v >> (8 * j)) & 0xFFu) * 4u);
+        x ^= t >= 0 ? e : 0u;
+    }
+    return x;
+}
+
 // One 128-B row: each lane folds its 16 bytes into its four chains.
 // All 16 addresses, then all 16 lookups, then the XORs, so a wave keeps 16
 // conflict-free ds_read_b32 in flight per row.
@@ -1957,6 +1973,7 @@ struct SortShared
     uint64_t pre[2];           // cost before those blocks
     uint64_t target[2];
     uint64_t wsum[kBlock / 64];
+    uint32_t zinv[1024];       // Z_{-128} (the finish pass)
 };
 constexpr uint32_t kLdsSorted = kLdsBytes + uint32_t((sizeof(SortShared) + 255) & ~size_t(255));
 static_assert(kLdsSorted <= 163840, "sorted kernel LDS");
@@ -2390,29 +2407,29 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
     const uint32_t* ones_word = tables + kTabFInit;  // Z_0(~0) = 0xFFFFFFFF
     const uint32_t* zneg = tables + kTabZNeg;
-    // An item is finished one group late: right after its fold, lane q < 4 of
-    // the team looks up byte q of the fold in the Z_{-m} table (one load per
-    // lane, issued with no wait); the next group's finish XORs the four
-    // entries and stores.  (Finishing at once drained the row ring.)
-    uint32_t pz = 0;               // this lane's Z_{-m} entry of the pending item
-    uint32_t p_recf = kSortNone;   // the pending item's record | flags
-    uint64_t p_pe = 0;             // its end (lane 0; split records only)
+    // A whole record's fold value goes to out[] right after its fold; the
+    // finish pass after the loop applies Z_{-m} from LDS tables.  (Round 2-3
+    // applied it in the loop from the 512 KB global Z_{-m} table, one lookup
+    // per lane a group later: 4M scattered L2 lines per configs[2] step,
+    // 10 us of it; profiles/r03_sorted_late_finish_ab.txt.)  Only a piece of
+    // a split record still takes that lookup in the loop: its part,
+    // Z_{E-pe}(raw(piece)), is XORed into out[] a group later.
+    uint32_t pz = 0;               // this lane's Z_{-m} entry of the pending piece
+    uint32_t p_recf = kSortNone;   // the pending piece's record | flags
+    uint64_t p_pe = 0;             // its end (lane 0)
+    bool p_multi = false;          // wave-uniform: some team has a pending piece
     auto flush = [&]() {
+        if (!p_multi) return;
         uint32_t v = pz;
         v ^= from_lane_up<1>(v);
-        v ^= from_lane_up<2>(v);  // lane 0: Z_{-m}(fold) = raw(item)
+        v ^= from_lane_up<2>(v);  // lane 0: Z_{-m}(fold) = raw(piece)
         if (tl == 0 && p_recf != kSortNone)
         {
+            // this piece's part: Z_{E - pe}(raw(piece)), E the record's end
             const uint32_t rec = p_recf & kSortRecMask;
-            if (!(p_recf & kSortMulti))
-                out[rec] = ~v;  // (non-temporal stores here: slower, partial lines)
-            else
-            {
-                // this piece's part: Z_{E - pe}(raw(piece)), E the record's end
-                const uint64_t E_rec = uint64_t(base) + off[rec] + len[rec];
-                v = zshift48(pow2, v, E_rec - p_pe);
-                __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            const uint64_t E_rec = uint64_t(base) + off[rec] + len[rec];
+            v = zshift48(pow2, v, E_rec - p_pe);
+            __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
     auto grab = [&]() {
@@ -2570,18 +2587,24 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         // the next group's row 1 if it has two rows (b[1] is free now)
         if (RB == 2 && shn.n == 2) b[1] = load16(row_ptr(nxt, 1, false));
         const uint32_t W = team_fold(V);
-        flush();  // the previous group's items
+        flush();  // the previous group's split-record pieces
         {
-            // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
-            const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
-            const uint32_t q = tl & 3u;
-            uint32_t pz_new = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
-            // an opaque definition: without it the loop-carried copy of pz at the
-            // loop header waited for this load (and the ring's row 0) every group
-            asm volatile("" : "+v"(pz_new));
-            pz = pz_new;
-            p_recf = cur.recf;
-            p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;  // lane 0: the item's end
+            const bool multi = cur.recf != kSortNone && (cur.recf & kSortMulti);
+            if (tl == 0 && cur.recf != kSortNone && !multi) out[cur.recf & kSortRecMask] = W;  // finish pass: Z_{-m}
+            p_multi = __builtin_amdgcn_ballot_w64(multi) != 0;
+            if (p_multi)
+            {
+                // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
+                const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
+                const uint32_t q = tl & 3u;
+                uint32_t pz_new = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
+                // an opaque definition: without it the loop-carried copy of pz at
+                // the loop header waited for this load every group
+                asm volatile("" : "+v"(pz_new));
+                pz = pz_new;
+            }
+            p_recf = multi ? cur.recf : kSortNone;
+            p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;
         }
         g_nxt = g_nn;
         d_nxt = d_nn;
@@ -2595,6 +2618,34 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
+    // Finish pass: the workgroup's whole records hold their fold value, the
+    // record's bytes followed by m = ceil128(E) - E zero bytes; raw = Z_{-m}
+    // of it, crc = ~raw.  (Split records were finished by their pieces' XORs.)
+    S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
+    __syncthreads();  // the workgroup's own stores are visible to it past the barrier
+    constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
+    for (uint64_t r = uint64_t(rlo) + threadIdx.x; r < rend; r += kBlock)
+    {
+        const uint64_t a = uint64_t(base) + off[r];
+        const uint32_t L = len[r];
+        const RecInfo f = info(r, a, L);
+        if (f.s.n == 1 && f.last)
+        {
+            // Z_{-m} = Z_{-128} Z_{128-m}, n = 128 - m = 64 a + 32 b + 16 c + rr
+            const uint32_t m = uint32_t(0u - uint32_t(a + L)) & 127u;
+            uint32_t v = out[r];
+            if (m)
+            {
+                const uint32_t n = 128u - m;
+                v = zT_n(v, n & 15u);
+                v = (n & 16u) ? zT<4>(v) : v;
+                v = (n & 32u) ? zG(kLdsZ32, v) : v;
+                v = (n & 64u) ? zG(kLdsZ64, v) : v;
+                v = zG(kLdsZInv, v);
+            }
+            out[r] = ~v;
+        }
+    }
 }
 
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,
