@@ -132,6 +132,7 @@ struct SortedWorkspace
     uint32_t* ctrl;      // 4 words: item cursor, overflow flag
     uint4* items;        // item_cap 16-B descriptors
     uint64_t item_cap;   // sorted_item_cap(count, total_bytes)
+    uint32_t* wr;        // item_cap words: a whole record's fold value, by descriptor slot
 };
 // batches of at least this many bytes (the total known) take the sorted path:
 // below it the piece path is 15-60 % faster, from it on the two are within

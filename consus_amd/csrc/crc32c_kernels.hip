@@ -2155,6 +2155,7 @@ struct SortView
     uint4 ke;        // row n - 1: keep masks (bytes before the item end)
     uint32_t m;      // bytes masked after the item in the last row
     uint32_t recf;   // record | flags, kSortNone: no item
+    uint32_t slot;   // the item's descriptor slot (whole records)
 };
 
 __device__ __forceinline__ uint32_t sort_rows(const uint4& d)
@@ -2228,7 +2229,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     const uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
-    uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ out,
+    uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2)
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
@@ -2304,6 +2305,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
         for (uint32_t i = 0; i < f.nf; ++i) put(fullv + S.full_base + fpos + i, desc(r, a, L, f, f.klo + i));
         if (f.last) put(lastv + lpos, desc(r, a, L, f, f.s.n - 1));
+        // a whole record's out[] holds its slot until the finish pass (whose
+        // record-order reads and stores are coalesced; the loop's fold value
+        // goes to wr[slot], contiguous in list order)
+        if (f.last && f.s.n == 1) out[r] = lpos;
     };
     uint64_t ha[CH][U];
     uint32_t hL[CH][U], hf[CH][U], hl[CH][U];
@@ -2488,6 +2493,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint4 d_nxt = load_desc(g_nxt);
     Shape shA = shape_of(d_cur, g_cur);
     SortView vA = sort_view(d_cur, shA.n, tl, inits, ones_word);
+    const uint32_t slot0 = rlo - n_full + tw;  // slot of list position i: slot0 + 8 g (whole records)
+    vA.slot = slot0 + g_cur * 8;
     Shape shB{0, 0, 0, 0};
     SortView vB = vA;
     const SortView& cur0 = vA;
@@ -2517,6 +2524,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const uint4 d_nn = load_desc(g_nn);
         shn = shape_of(d_nxt, g_nxt);
         nxt = sort_view(d_nxt, shn.n, tl, inits, ones_word);
+        nxt.slot = slot0 + g_nxt * 8;
         uint32_t V[4] = {0, 0, 0, 0};
         const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
         // General row: padding skip, start mask and init word (rows up to
@@ -2590,7 +2598,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         flush();  // the previous group's split-record pieces
         {
             const bool multi = cur.recf != kSortNone && (cur.recf & kSortMulti);
-            if (tl == 0 && cur.recf != kSortNone && !multi) out[cur.recf & kSortRecMask] = W;  // finish pass: Z_{-m}
+            // whole records: the fold value by slot, eight consecutive words per
+            // group (stores to out[rec] here hit a line per record, scattered:
+            // 8-11 us of the configs[2] step, profiles/r03_sorted_late_finish_ab.txt)
+            if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
             p_multi = __builtin_amdgcn_ballot_w64(multi) != 0;
             if (p_multi)
             {
@@ -2618,9 +2629,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
-    // Finish pass: the workgroup's whole records hold their fold value, the
-    // record's bytes followed by m = ceil128(E) - E zero bytes; raw = Z_{-m}
-    // of it, crc = ~raw.  (Split records were finished by their pieces' XORs.)
+    // Finish pass, in record order: a whole record's fold value (wr at its
+    // slot) is Z_m(raw) of its bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).
+    // (Split records were finished by their pieces' XORs.)
     S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     __syncthreads();  // the workgroup's own stores are visible to it past the barrier
     constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
@@ -2633,7 +2644,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             // Z_{-m} = Z_{-128} Z_{128-m}, n = 128 - m = 64 a + 32 b + 16 c + rr
             const uint32_t m = uint32_t(0u - uint32_t(a + L)) & 127u;
-            uint32_t v = out[r];
+            uint32_t v = wr[uint64_t(rlo) + out[r]];  // out[r]: the record's slot - rlo
             if (m)
             {
                 const uint32_t n = 128u - m;
@@ -2660,7 +2671,7 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
                        lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables);
     hipLaunchKernelGGL(crc32c_sorted_kernel, dim3(grid), dim3(kBlock), kLdsSorted, stream, b,
                        offsets, lengths, inits, count, ws.blk_cost, nb, ws.ctrl, ws.items,
-                       ws.item_cap, out, tables, pow2);
+                       ws.item_cap, ws.wr, out, tables, pow2);
     return hipGetLastError();
 }
 

@@ -525,11 +525,15 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     // + a stamp area for MI_SORT_STAMP measurement builds (8 words per wave);
     // ctrl: 64 words, then one 256-B slot per workgroup (MI_SORT_GGRAB builds)
     if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
-        (st = c->srt_ctrl.reserve(4 * (64 + 64 * uint64_t(8 * d->cus)))) || (st = c->srt_items.reserve(cap * 16 + 65536 * 64)))
+        (st = c->srt_ctrl.reserve(4 * (64 + 64 * uint64_t(8 * d->cus)))) ||
+        (st = c->srt_items.reserve(cap * 20 + 65536 * 64)))
         return st;
+    // descriptors, then the stamp area, then the fold values by slot
+    uint8_t* const ib = c->srt_items.as<uint8_t>();
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
-                       c->srt_items.as<uint4>(), (c->srt_items.cap - 65536 * 64) / 16};
-    last_sorted_stamps = reinterpret_cast<uint64_t*>(ws.items + ws.item_cap);
+                       reinterpret_cast<uint4*>(ib), cap,
+                       reinterpret_cast<uint32_t*>(ib + cap * 16 + 65536 * 64)};
+    last_sorted_stamps = reinterpret_cast<uint64_t*>(ib + cap * 16);
     // MI_CRC32C_SORTED_GRID=k: k workgroups instead of one per CU (tests: one
     // workgroup puts every item of a small batch into one sorted list)
     int grid = d->cus;
