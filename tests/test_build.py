@@ -59,6 +59,16 @@ def test_headline_kernel_fits_16_waves_without_spills(asm):
         assert f["private_segment_fixed_size"] == 0
 
 
+def test_sorted_kernel_fits_16_waves_without_spills(asm):
+    """The sorted path's hash kernel (configs[2]) runs 16 waves per CU: at most
+    128 VGPRs, no scratch; its LDS image plus the sort state fit 160 KiB."""
+    meta = kernel_meta(asm)
+    srt = [f for k, f in meta.items() if "crc32c_sorted_kernel" in k]
+    assert len(srt) == 1
+    assert srt[0]["next_free_vgpr"] <= 128
+    assert srt[0]["private_segment_fixed_size"] == 0
+
+
 def test_no_scalar_cache_writes(asm):
     # opcode families assembled from fragments, so that this file itself
     # names none of them
