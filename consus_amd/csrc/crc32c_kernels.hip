@@ -2635,26 +2635,47 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     __syncthreads();  // the workgroup's own stores are visible to it past the barrier
     constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
-    for (uint64_t r = uint64_t(rlo) + threadIdx.x; r < rend; r += kBlock)
+    // four records per thread per round: every load of the round issued
+    // before any is used (the pass is two dependent global round trips and
+    // five LDS rounds per record; round 3 A/B: -1 to -2 us against one record
+    // per round, profiles/r03_sorted_late_finish_ab.txt)
+    constexpr uint32_t FU = 4;
+    for (uint64_t r0 = uint64_t(rlo) + threadIdx.x; r0 < rend; r0 += FU * kBlock)
     {
-        const uint64_t a = uint64_t(base) + off[r];
-        const uint32_t L = len[r];
-        const RecInfo f = info(r, a, L);
-        if (f.s.n == 1 && f.last)
+        uint64_t av[FU];
+        uint32_t Lv[FU], sv[FU];
+#pragma unroll
+        for (uint32_t u = 0; u < FU; ++u)
         {
-            // Z_{-m} = Z_{-128} Z_{128-m}, n = 128 - m = 64 a + 32 b + 16 c + rr
-            const uint32_t m = uint32_t(0u - uint32_t(a + L)) & 127u;
-            uint32_t v = wr[uint64_t(rlo) + out[r]];  // out[r]: the record's slot - rlo
-            if (m)
-            {
-                const uint32_t n = 128u - m;
-                v = zT_n(v, n & 15u);
-                v = (n & 16u) ? zT<4>(v) : v;
-                v = (n & 32u) ? zG(kLdsZ32, v) : v;
-                v = (n & 64u) ? zG(kLdsZ64, v) : v;
-                v = zG(kLdsZInv, v);
-            }
-            out[r] = ~v;
+            const uint64_t r = r0 + u * kBlock;
+            const bool in = r < rend;
+            av[u] = uint64_t(base) + (in ? off[r] : 0);
+            Lv[u] = in ? len[r] : 0u;
+            sv[u] = in ? out[r] : 0u;
+        }
+        uint32_t wv[FU];
+        bool own[FU];
+#pragma unroll
+        for (uint32_t u = 0; u < FU; ++u)
+        {
+            const uint64_t r = r0 + u * kBlock;
+            const RecInfo f = info(r, av[u], Lv[u]);
+            own[u] = r < rend && f.s.n == 1 && f.last;
+            wv[u] = own[u] ? wr[uint64_t(rlo) + sv[u]] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < FU; ++u)
+        {
+            const uint32_t m = uint32_t(0u - uint32_t(av[u] + Lv[u])) & 127u;
+            uint32_t v = wv[u];
+            const uint32_t n = 128u - m;
+            uint32_t t = zT_n(v, n & 15u);
+            t = (n & 16u) ? zT<4>(t) : t;
+            t = (n & 32u) ? zG(kLdsZ32, t) : t;
+            t = (n & 64u) ? zG(kLdsZ64, t) : t;
+            t = zG(kLdsZInv, t);
+            v = m ? t : v;
+            if (own[u]) out[r0 + u * kBlock] = ~v;
         }
     }
 }
