@@ -20,6 +20,7 @@
 #include <fcntl.h>
 #include <pthread.h>
 #include <signal.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/file.h>
@@ -354,6 +355,11 @@ durable_log::durable_log(const durable_log_options& options)
     , m_segment_a(nullptr)
     , m_segment_b(nullptr)
     , m_active(nullptr)
+    , m_switch_gen(0)
+    , m_flush_phase(0)
+    , m_slow_waiters(0)
+    , m_append_hook(nullptr)
+    , m_append_hook_ctx(nullptr)
     , m_durable(1)
     , m_flush_idle(false)
     , m_crc(gpu_batch)
@@ -451,6 +457,44 @@ void durable_log::note_phase(int phase, uint64_t ns)
 void durable_log::set_fsync_delay_for_testing(uint32_t microseconds)
 {
     m_fsync_delay_us.store(microseconds);
+}
+
+void durable_log::set_append_hook_for_testing(void (*fn)(void*, int), void* ctx)
+{
+    std::lock_guard<std::mutex> hold(m_mtx);
+    if (m_opened) return;
+    m_append_hook = fn;
+    m_append_hook_ctx = ctx;
+}
+
+void durable_log::debug_state(char* buf, size_t n)
+{
+    if (!buf || !n) return;
+    static const char* const phases[] = {"start",     "idle",        "sealing", "wait-copies",
+                                         "prepare",   "wait-spare",  "stopped"};
+    std::lock_guard<std::mutex> hold(m_mtx);
+    const segment* act = m_active.load();
+    const int ph = m_flush_phase.load();
+    uint64_t w = 0, staged = 0, failed = 0, base = 0;
+    if (act)
+    {
+        w = act->word.load();
+        staged = act->done_total();
+        failed = act->failed.load();
+        base = act->base;
+    }
+    snprintf(buf, n,
+             "flush=%s active=%s sealed=%d frames=%llu bytes=%llu staged=%llu failed=%llu "
+             "base=%llu switches=%llu flush_idle=%d spare=%d jobs=%zu pending=%zu "
+             "append_slow=%d error=%d durable=%llu",
+             ph >= 0 && ph <= 6 ? phases[ph] : "?",
+             !act ? "none" : act == m_segment_a ? "a" : "b", int((w & kSealed) != 0),
+             (unsigned long long)((w & ~kSealed) >> kIdxShift),
+             (unsigned long long)(w & kUsedMask), (unsigned long long)staged,
+             (unsigned long long)failed, (unsigned long long)base,
+             (unsigned long long)m_switch_gen.load(), int(m_flush_idle.load()),
+             int(m_spare != nullptr), m_jobs.size(), m_pending.size(), m_slow_waiters.load(),
+             m_error.load(), (unsigned long long)m_durable.load());
 }
 
 bool durable_log::open(const std::string& dir)
@@ -615,12 +659,17 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
             errno = e;
             return -1;
         }
+        // the generation first: switch_to_next stores m_active before it
+        // bumps the generation, so seg is the segment of generation `gen` or
+        // a later one, and a switch away from seg always moves it past gen
+        const uint64_t gen = m_switch_gen.load(std::memory_order_acquire);
         segment* seg = m_active.load(std::memory_order_acquire);
         if (!seg)
         {
             errno = EBADF;
             return -1;
         }
+        if (m_append_hook) m_append_hook(m_append_hook_ctx, 0);
         // record number and staging offset in one step (txman/durable_log.cc:
         // 195-213 takes m_mtx for the same reservation)
         const uint64_t w = seg->word.fetch_add((uint64_t(1) << kIdxShift) | arena_bytes);
@@ -682,7 +731,8 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
             seg->failed.fetch_add(1, std::memory_order_release);
         }
         // sealed (the flush thread is switching segments) or full
-        const int64_t r = append_slow(seg);
+        if (m_append_hook) m_append_hook(m_append_hook_ctx, 1);
+        const int64_t r = append_slow(seg, gen);
         if (r < 0) return r;
     }
 }
@@ -690,11 +740,23 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
 // The active segment is full or being sealed: wake the flush thread and wait
 // until it has switched appends to the other segment (backpressure when both
 // staging buffers are in use, as the reference's writers wait on its flush).
-int64_t durable_log::append_slow(segment* seg)
+// A segment sealed or filled at generation `gen` is always followed by a
+// switch (the flush thread seals only the active segment, and switches away
+// from it once its reservations are accounted for), so waiting for the
+// generation to move cannot block forever.  Waiting for m_active != seg could:
+// two switches (seg -> other -> seg) between this appender's failed
+// reservation and its wait bring seg back, empty, and with no other appender
+// the flush thread then sleeps on it for good.  txman/durable_log.cc:195-213
+// never waits for a switch (its segment files are unbounded); here the
+// staging arenas are bounded, so a full one is backpressure.
+int64_t durable_log::append_slow(segment* seg, uint64_t gen)
 {
     std::unique_lock<std::mutex> hold(m_mtx);
-    m_cond.notify_all();
-    m_cond.wait(hold, [&] { return m_error != 0 || m_active.load() != seg; });
+    // wake the flush thread only if seg is still the one to switch away from
+    if (m_switch_gen.load() == gen && m_active.load() == seg) m_cond.notify_all();
+    ++m_slow_waiters;
+    m_cond.wait(hold, [&] { return m_error != 0 || m_switch_gen.load() != gen; });
+    --m_slow_waiters;
     if (m_error != 0)
     {
         errno = m_error;
@@ -1005,6 +1067,7 @@ void durable_log::switch_to_next(segment* seg, uint64_t n)
     next->cut.store(~uint64_t(0));
     next->word.store(0);  // unsealed, empty: appends may reserve in it
     m_active.store(next);
+    m_switch_gen.fetch_add(1);  // after m_active: see append()
     m_cond.notify_all();  // appenders waiting for room
 }
 
@@ -1053,9 +1116,14 @@ void durable_log::flush()
         bool exact = true;
         {
             std::unique_lock<std::mutex> hold(m_mtx);
+            m_flush_phase.store(1);
             while (true)
             {
-                if (m_error != 0) return;
+                if (m_error != 0)
+                {
+                    m_flush_phase.store(6);
+                    return;
+                }
                 seg = m_active.load();
                 if (seg)
                 {
@@ -1068,6 +1136,7 @@ void durable_log::flush()
                 m_cond.wait(hold);
             }
             m_flush_idle.store(false);
+            m_flush_phase.store(2);
             // seal.  Unless the segment filled up, every reservation taken
             // so far is valid, so appends move to the other segment at once,
             // before the copies into this one finish.
@@ -1079,6 +1148,7 @@ void durable_log::flush()
         }
         // every reservation taken before the seal finishes: its frame is
         // staged, or it did not fit (and its appender retries elsewhere)
+        m_flush_phase.store(3);
         const auto t_wait = std::chrono::steady_clock::now();
         for (int spins = 0; seg->done_total() + seg->failed.load(std::memory_order_acquire) != n;
              ++spins)
@@ -1104,6 +1174,7 @@ void durable_log::flush()
             std::lock_guard<std::mutex> hold(m_mtx);
             switch_to_next(seg, n);
         }
+        m_flush_phase.store(4);
         auto* job = new write_job;
         const int e = prepare_segment(seg, n, used, job);
         {
@@ -1111,17 +1182,20 @@ void durable_log::flush()
             if (e)
             {
                 m_error = e;
+                m_flush_phase.store(6);
                 m_cond.notify_all();
                 hold.unlock();
                 delete job;
                 return;
             }
+            m_flush_phase.store(5);
             // hand the bytes to the writer in their arena; the segment takes
             // the spare one (back from the writer's previous job) before it
             // can be active again
             m_cond.wait(hold, [&] { return m_error != 0 || m_spare != nullptr; });
             if (m_error != 0)
             {
+                m_flush_phase.store(6);
                 hold.unlock();
                 delete job;
                 return;
@@ -1247,6 +1321,11 @@ void mi_dlog_set_fsync_delay_for_testing(mi_dlog* l, uint32_t microseconds)
 {
     l->log.set_fsync_delay_for_testing(microseconds);
 }
+void mi_dlog_set_append_hook_for_testing(mi_dlog* l, void (*fn)(void*, int), void* ctx)
+{
+    l->log.set_append_hook_for_testing(fn, ctx);
+}
+void mi_dlog_debug_state(mi_dlog* l, char* buf, size_t n) { l->log.debug_state(buf, n); }
 
 int64_t mi_dlog_scan_file(const char* path, uint64_t* valid_bytes, uint64_t* recnos,
                           uint64_t* offsets, size_t max_frames)

@@ -32,6 +32,7 @@ _SIGS = {
     "mi_dlog_external_peak": (C.c_uint64, [C.c_void_p]),
     "mi_dlog_set_batch_crc_for_testing": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "mi_dlog_set_fsync_delay_for_testing": (None, [C.c_void_p, C.c_uint32]),
+    "mi_dlog_debug_state": (None, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "mi_dlog_flush_seconds": (None, [C.c_void_p, C.POINTER(C.c_double)]),
     "mi_dlog_scan_file": (C.c_int64, [C.c_char_p, C.POINTER(C.c_uint64), C.c_void_p, C.c_void_p,
                                       C.c_size_t]),
@@ -113,6 +114,14 @@ class DurableLog:
 
     def set_fsync_delay_for_testing(self, microseconds: int) -> None:
         _lib().mi_dlog_set_fsync_delay_for_testing(self._h, int(microseconds))
+
+    def debug_state(self) -> str:
+        """One line of internal state (flush-thread phase, the active
+        segment's reservation word, queued jobs, appenders waiting for a
+        switch); for watchdogs."""
+        buf = C.create_string_buffer(512)
+        _lib().mi_dlog_debug_state(self._h, buf, len(buf))
+        return buf.value.decode()
 
     def destroy(self) -> None:
         if self._h:

@@ -38,7 +38,8 @@ int64_t mi_dlog_replay(mi_dlog* log, void (*f)(void*, const unsigned char*, size
 uint64_t mi_dlog_flushes(mi_dlog* log);
 uint64_t mi_dlog_frames_flushed(mi_dlog* log);
 /* most bytes of oversized frames (more than half a segment, staged outside
- * the arenas) held at once: bounded by max(segment capacity, largest frame) */
+ * the arenas) held at once: bounded by max(2 x segment capacity, 16 MiB,
+ * largest frame) */
 uint64_t mi_dlog_external_peak(mi_dlog* log);
 /* Seconds the flush thread has spent, summed over flushes, in: [0] waiting
  * for in-flight appends of a sealed segment, [1] walking the frame chain,
@@ -55,6 +56,15 @@ typedef int (*mi_dlog_batch_crc)(void* ctx, const void* base, const uint64_t* of
 void mi_dlog_set_batch_crc_for_testing(mi_dlog* log, mi_dlog_batch_crc fn, void* ctx);
 /* Test hook: every fsync also sleeps this long (a slow disk on tmpfs). */
 void mi_dlog_set_fsync_delay_for_testing(mi_dlog* log, uint32_t microseconds);
+/* Test hook (call before open): every append calls fn(ctx, 0) after reading
+ * the active segment, before reserving in it, and fn(ctx, 1) after a failed
+ * reservation (segment sealed or full), before waiting for the switch. */
+void mi_dlog_set_append_hook_for_testing(mi_dlog* log, void (*fn)(void* ctx, int point),
+                                         void* ctx);
+/* One line of internal state for watchdogs (flush-thread phase, the active
+ * segment's reservation word, staged / failed frames, queued jobs, appenders
+ * waiting for a segment switch); at most n bytes including the NUL. */
+void mi_dlog_debug_state(mi_dlog* log, char* buf, size_t n);
 
 /* Segment verifier (the reference's missing replay, TODO:2-3): parse the
  * frames of one segment file by their length chain and verify every CRC in

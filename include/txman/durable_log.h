@@ -97,8 +97,20 @@ class __attribute__((visibility("default"))) durable_log
         // Test hook: every fsync also sleeps this long (a slow disk on tmpfs).
         void set_fsync_delay_for_testing(uint32_t microseconds);
         // Most bytes of oversized frames (staged outside the arenas) held at
-        // once: at most max(segment capacity, the largest such frame).
+        // once: at most max(2 x segment capacity, 16 MiB, the largest such
+        // frame).
         uint64_t external_bytes_peak() const;
+        // Test hook (call before open): every append calls fn(ctx, point) at
+        // point 0, after it has read the active segment and before it
+        // reserves in it, and at point 1, after a reservation that failed
+        // (segment sealed or full) and before it waits for the flush thread
+        // to switch segments.  A test parks one appender there while the
+        // flush thread switches segments under it.
+        void set_append_hook_for_testing(void (*fn)(void* ctx, int point), void* ctx);
+        // One line of the log's internal state (flush-thread phase, the
+        // active segment's reservation word, queued jobs, appenders waiting
+        // for a switch) for watchdogs; writes at most n bytes, NUL included.
+        void debug_state(char* buf, size_t n);
 
     private:
         struct segment;
@@ -113,7 +125,7 @@ class __attribute__((visibility("default"))) durable_log
         void warm_up();
         void writer();
         void sync();
-        int64_t append_slow(segment* seg);
+        int64_t append_slow(segment* seg, uint64_t gen);
         void switch_to_next(segment* seg, uint64_t n);
         int prepare_segment(segment* seg, uint64_t& nframes, uint64_t& used, write_job* job);
         int write_out(write_job* job);
@@ -140,6 +152,15 @@ class __attribute__((visibility("default"))) durable_log
         segment* m_segment_a;
         segment* m_segment_b;
         std::atomic<segment*> m_active;      // the segment appends reserve in
+        // segment switches so far, bumped after m_active is stored: an
+        // appender that saw generation g and a sealed or full segment waits
+        // for a generation != g (waiting on m_active != seg was ABA-prone:
+        // two switches bring the same segment back)
+        std::atomic<uint64_t> m_switch_gen;
+        std::atomic<int> m_flush_phase;      // what the flush thread is doing (debug_state)
+        std::atomic<int> m_slow_waiters;     // appenders waiting for a switch (debug_state)
+        void (*m_append_hook)(void*, int);   // test hook, set before open()
+        void* m_append_hook_ctx;
         std::atomic<uint64_t> m_durable;     // every recno below it is on disk
         std::atomic<bool> m_flush_idle;      // the flush thread sleeps for a first frame
         durable_log_batch_crc m_crc;

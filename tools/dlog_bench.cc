@@ -176,15 +176,18 @@ int main(int argc, char** argv)
                 double f[6], m[6];
                 log.flush_seconds(f);
                 log.flush_max_seconds(m);
+                char st_line[512];
+                log.debug_state(st_line, sizeof st_line);
                 fprintf(stderr,
                         "dlog_bench: stage '%s' exceeded %.0f s: durable %lld, flushes %llu, frames "
                         "flushed %llu, error %d; flush s: wait %.3f walk %.3f crc %.3f patch %.3f "
-                        "pwrite %.3f fsync %.3f; max us: %.0f %.0f %.0f %.0f %.0f %.0f\n",
+                        "pwrite %.3f fsync %.3f; max us: %.0f %.0f %.0f %.0f %.0f %.0f\n"
+                        "dlog_bench: state: %s\n",
                         kStage[st], wd_limit, (long long)log.durable(),
                         (unsigned long long)log.flushes(),
                         (unsigned long long)log.frames_flushed(), log.error(), f[0], f[1], f[2],
                         f[3], f[4], f[5], m[0] * 1e6, m[1] * 1e6, m[2] * 1e6, m[3] * 1e6,
-                        m[4] * 1e6, m[5] * 1e6);
+                        m[4] * 1e6, m[5] * 1e6, st_line);
                 fflush(stderr);
                 _exit(3);
             }
