@@ -1076,8 +1076,9 @@ void durable_log::switch_to_next(segment* seg, uint64_t n)
 // open, before the first frame can wait for it: inside the first flush it
 // was the p99 of the durability latency (7-14 ms against < 1 ms with the CPU
 // checksum, round 3).  One 64-B record of the spare arena (pinned, unused
-// until the first flush returns it to the writer), result ignored; no
-// fallback flag, so a host without a device counts nothing.
+// until the first flush returns it to the writer) per device the flush may
+// use, result ignored; no fallback flag, so a host without a device counts
+// nothing.
 void durable_log::warm_up()
 {
     const unsigned char* arena = nullptr;
@@ -1090,7 +1091,22 @@ void durable_log::warm_up()
     const uint64_t off = 0;
     const uint32_t len = 64;
     uint32_t out = 0;
-    (void)mi_crc32c_batch(arena, &off, &len, nullptr, 1, len, &out, 0);
+    if (m_opts.gpus == 1)
+    {
+        (void)mi_crc32c_batch(arena, &off, &len, nullptr, 1, len, &out, 0);
+        return;
+    }
+    // A sharded flush runs its extra ranges on the engine's worker threads,
+    // each with its own per-thread, per-device context: warm all of them
+    // through the same entry point and device list (one 64-B record per
+    // device, forced to split with a 1-byte shard minimum).
+    const int nd = std::max(mi_crc32c_device_count(), 1);
+    std::vector<uint64_t> offs(size_t(nd), 0);
+    std::vector<uint32_t> lens(size_t(nd), len);
+    std::vector<uint32_t> outs(size_t(nd), 0);
+    (void)mi_crc32c_batch_multi(arena, offs.data(), lens.data(), nullptr, size_t(nd),
+                                uint64_t(len) * uint64_t(nd), outs.data(), 0, nullptr,
+                                m_opts.gpus, 1);
 }
 
 // The flush thread (txman/durable_log.cc:287-347): wait for a first staged

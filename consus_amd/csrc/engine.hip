@@ -390,6 +390,16 @@ struct Ctx
             }
         }
         HIP_TRY(hipStreamSynchronize(stream));
+        if (signalled && *static_cast<const volatile uint32_t*>(pin_small.as<uint32_t>() +
+                                                                kDoneWord) != done_seq)
+        {
+            // The launch finished without storing its word: its counter did
+            // not end at the grid size (a launch cut short), and only the
+            // last workgroup resets it.  Zero it here, so the next launch's
+            // last workgroup cannot fire before every CRC is stored.
+            HIP_TRY(hipMemsetAsync(done_ctr.p, 0, 64, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+        }
         return MI_CRC32C_OK;
     }
     // Waits for the stream's work, then frees every buffer, event and the stream.
@@ -482,15 +492,38 @@ const uint8_t* mapped_device_ptr(const void* p)
            (static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(a.hostPointer));
 }
 
-bool is_pinned(const void* p)
+// The device's address of the span [p, p + n) if ALL of it is in mapped
+// pinned memory, read through one contiguous device mapping; else null (the
+// batch is then staged by a CPU copy, which only needs the span readable).
+// Checking the first byte alone let a span that runs from a mapped buffer
+// into pageable memory reach the kernel, which would then read past the
+// mapping.  Both ends must be mapped, at device addresses the
+// same distance apart; when the runtime reports the device allocation's
+// range, the span's end must lie inside it too.
+const uint8_t* mapped_span_device_ptr(const uint8_t* p, uint64_t n)
 {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess)
+    const uint8_t* d0 = mapped_device_ptr(p);
+    if (!d0 || n <= 1) return d0;
+    const uint8_t* d1 = mapped_device_ptr(p + (n - 1));
+    if (!d1 || d1 < d0 || uint64_t(d1 - d0) != n - 1) return nullptr;
+    hipDeviceptr_t pbase = nullptr;
+    size_t psize = 0;
+    if (hipMemGetAddressRange(&pbase, &psize, const_cast<uint8_t*>(d0)) == hipSuccess)
     {
-        (void)hipGetLastError();
-        return false;
+        const uint8_t* b = static_cast<const uint8_t*>(pbase);
+        if (d0 < b || uint64_t(d1 - b) >= psize) return nullptr;
     }
-    return a.type == hipMemoryTypeHost;
+    else
+        (void)hipGetLastError();
+    return d0;
+}
+
+// All of [p, p + n) is pinned host memory of one mapping, so a copy engine
+// may read it in place (pinned-but-unmapped spans take the CPU copy: correct,
+// only slower).
+bool is_pinned_span(const void* p, uint64_t n)
+{
+    return mapped_span_device_ptr(static_cast<const uint8_t*>(p), n) != nullptr;
 }
 
 uint32_t apply_zeros(const DeviceState* d, uint32_t s, uint64_t n)
@@ -794,7 +827,8 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
     if (hi > lo && maxlen_arg <= kDirectMaxRecord && total <= kDirectMaxBytes &&
         count <= kDirectMaxCount && !zero_copy_disabled())
     {
-        if (const uint8_t* zsrc = mapped_device_ptr(static_cast<const uint8_t*>(base) + lo))
+        if (const uint8_t* zsrc = mapped_span_device_ptr(static_cast<const uint8_t*>(base) + lo,
+                                                         hi - lo))
         {
             const uint64_t meta_bytes = uint64_t(count) * (inits ? 16 : 12);
             if ((st = c->pin_stage.reserve(meta_bytes + 16)) || (st = c->pin_out.reserve(count * 4)))
@@ -833,7 +867,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
     // CPU copy into the packed buffer beats a second copy command (measured:
     // 400 frames, 227 KB: 50 us packed vs 54 us with the bytes DMA'd in place)
     const bool src_pinned = hi - lo > kPackInPlace &&
-                            is_pinned(static_cast<const uint8_t*>(base) + lo);
+                            is_pinned_span(static_cast<const uint8_t*>(base) + lo, hi - lo);
     const uint64_t data_at = (meta + 127) & ~uint64_t(127);
     const uint64_t packed = data_at + (src_pinned ? 0 : hi - lo);
     if (packed <= kPackMax)
@@ -1172,7 +1206,7 @@ int mi_crc32c_pipeline_submit(mi_crc32c_pipeline* p, const void* host_segment, s
     int st;
     if ((st = slot_complete(s))) return st;
     const void* src = host_segment;
-    if (bytes && !is_pinned(host_segment))
+    if (bytes && !is_pinned_span(host_segment, bytes))
     {
         std::memcpy(s.seg.p, host_segment, bytes);
         src = s.seg.p;

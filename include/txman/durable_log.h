@@ -23,6 +23,11 @@
 // watermark still covers only records whose CRC bytes are on disk.  The
 // fsync of one segment overlaps the CRC and write of the next (at most one
 // written segment waits for its fsync).
+// Errors: as in the reference, whose flush thread stops at the first error
+// (:226-230, :287-347), the first error -- an I/O error, or ENOMEM when an
+// oversized frame's own staging buffer cannot be allocated -- stops the log:
+// later appends fail, segments not yet fsynced are dropped, and the
+// watermark never passes the record that failed.
 // replay() -- declared but never defined by the reference (:64, TODO:2-3) --
 // is implemented as a GPU-verified scan of both segment files.
 #ifndef consus_txman_log_h_

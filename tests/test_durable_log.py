@@ -404,3 +404,35 @@ def test_slow_fsync_overlaps_next_write(make_log, tmp_path):
     assert secs[5] >= 0.003 * log.flushes() * 0.9  # the delayed fsyncs, on the sync thread
     log.close()
     assert log.replay() == [got[i] for i in range(1, 1001)]
+
+
+def test_watermark_never_passes_a_failed_record(make_log, tmp_path):
+    """an append whose staging malloc fails (an entry larger than
+    the address space) puts the log into ENOMEM.  As in the reference, whose
+    flush thread stops at the first error (txman/durable_log.cc:226-230,
+    287-347), segments not yet fsynced are then dropped: the watermark never
+    passes the failed record, later appends fail, and the files hold a
+    contiguous, CRC-valid prefix of the records before it."""
+    import errno
+    import time
+
+    from consus_amd.durable_log import _lib
+    log = make_log(capacity=1 << 16)
+    assert log.open(str(tmp_path / "d"))
+    entries = [bytes([i % 251]) * (40 + i) for i in range(60)]
+    for i, e in enumerate(entries[:50]):
+        assert log.append(e) == i + 1
+    wait_durable(log, 50)
+    for i, e in enumerate(entries[50:]):
+        assert log.append(e) == 51 + i
+    assert _lib().mi_dlog_append(log._h, b"x", 1 << 50) == -1
+    assert log.error() == errno.ENOMEM
+    t0 = time.time()
+    while time.time() - t0 < 0.3:
+        assert log.durable() <= 61
+        time.sleep(0.01)
+    assert log.append(b"after") == -1
+    log.close()
+    got = log.replay()
+    assert 50 <= len(got) <= 60
+    assert got == entries[:len(got)]

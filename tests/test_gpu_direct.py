@@ -102,3 +102,56 @@ def test_direct_tiny_packed_batches(engine, oracle, monkeypatch):
         offs = rng.integers(0, buf.size - 100, n).astype(np.uint64)
         got = engine.crc32c_batch(buf, offs, lens)
         assert np.array_equal(got, oracle.batch(buf, offs, lens, threads=1)), k
+
+
+def _hip():
+    import ctypes as C
+    for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+        try:
+            lib = C.CDLL(name)
+            break
+        except OSError:
+            continue
+    lib.hipHostRegister.restype = C.c_int
+    lib.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+    lib.hipHostUnregister.restype = C.c_int
+    lib.hipHostUnregister.argtypes = [C.c_void_p]
+    return lib
+
+
+def test_zero_copy_needs_the_whole_span_mapped(engine, oracle):
+    """a host batch whose span starts in mapped pinned
+    memory but runs on into pageable memory must not be read in place (the
+    kernel would read past the mapping); it is staged, bit-exact.  A batch
+    wholly inside the mapped part still is read in place.  The mapped part
+    is the first 1 MiB of a 2 MiB anonymous mapping, registered with
+    hipHostRegister(Mapped | Portable); the rest stays pageable."""
+    import mmap
+
+    hip = _hip()
+    size, half = 2 << 20, 1 << 20
+    mm = mmap.mmap(-1, size)
+    buf = np.frombuffer(mm, dtype=np.uint8)
+    rng = np.random.default_rng(95)
+    buf[:] = rng.integers(0, 256, size, dtype=np.uint8)
+    addr = buf.ctypes.data
+    assert hip.hipHostRegister(addr, half, 0x3) == 0
+    try:
+        # inside the mapped half: zero-copy
+        off = np.arange(64, dtype=np.uint64) * 4096 + 100
+        ln = np.full(64, 3000, dtype=np.uint32)
+        before = engine.stats()["zero_copy_batches"]
+        assert np.array_equal(engine.crc32c_batch(buf, off, ln), oracle.batch(buf, off, ln))
+        assert engine.stats()["zero_copy_batches"] - before == 1
+        # the same records plus one that crosses into the pageable half, and
+        # one wholly in it: staged, not zero-copy
+        for extra in ((half - 1000, 5000), (half + 300000, 9000)):
+            off2 = np.append(off, np.uint64(extra[0]))
+            ln2 = np.append(ln, np.uint32(extra[1]))
+            before = engine.stats()["zero_copy_batches"]
+            assert np.array_equal(engine.crc32c_batch(buf, off2, ln2),
+                                  oracle.batch(buf, off2, ln2)), extra
+            assert engine.stats()["zero_copy_batches"] == before, extra
+    finally:
+        assert hip.hipHostUnregister(addr) == 0
+        del buf

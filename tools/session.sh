@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-3 GPU session (dev tool): the GPU suite, then the measurement probes
+# GPU session (dev tool): the GPU suite, then the measurement probes
 # named on the command line.  Every GPU step has its own limit; the script
-# stops at the first failure.  Output: gpurun_out/r03/<step>.*
-#   tools/r03_session.sh tests route crossover rehearsal dlog zipf fixed ...
+# stops at the first failure.  Output: gpurun_out/$SESSION/<step>.* (SESSION default r04)
+#   tools/session.sh tests route crossover rehearsal dlog zipf fixed ...
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$ROOT/gpurun_out/r03"
+OUT="$ROOT/gpurun_out/${SESSION:-r04}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT" || exit 9
