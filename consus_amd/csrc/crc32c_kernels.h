@@ -133,15 +133,12 @@ struct SortedWorkspace
     uint4* items;        // item_cap 16-B descriptors
     uint64_t item_cap;   // sorted_item_cap(count, total_bytes)
     uint32_t* wr;        // item_cap words: a whole record's fold value, by descriptor slot
+    uint32_t plog;       // log2 of the piece records longer than it are cut into (9..16)
 };
-// batches of at least this many bytes (the total known) take the sorted path:
-// below it the piece path is 15-60 % faster, from it on the two are within
-// +-4 % up to ~2 GiB and the sorted path wins at configs[2]'s 4.9 GB
-// (tools/varpath_crossover.py, profiles/r03_varpath_crossover.txt)
-constexpr uint64_t kSortedMinBytes = 512ull << 20;
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);
-uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes);
+constexpr uint32_t kSortPieceLog2 = 16;  // 64 KiB pieces (the default)
+uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog);
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, const SortedWorkspace& ws,
                          uint32_t* out, const uint32_t* tables, const uint32_t* pow2, int grid,

@@ -1877,13 +1877,14 @@ struct SortCost
     uint32_t rows_last;
 };
 
-__device__ __forceinline__ SortCost sort_cost(uint64_t a, uint32_t L)
+__device__ __forceinline__ SortCost sort_cost(uint64_t a, uint32_t L, uint32_t plog)
 {
     SortCost s{0, 0, 0, 0, 0};
     if (L < 4) return s;
-    s.n = uint32_t((uint64_t(L) + kSortPiece - 1) / kSortPiece);
-    s.rows_full = uint32_t(kSortPiece / kRowBytes) + ((a & (kRowBytes - 1)) ? 1u : 0u);
-    const uint64_t ps = a + uint64_t(s.n - 1) * kSortPiece, E = a + L;
+    const uint64_t piece = uint64_t(1) << plog;
+    s.n = uint32_t((uint64_t(L) + piece - 1) >> plog);
+    s.rows_full = uint32_t(piece / kRowBytes) + ((a & (kRowBytes - 1)) ? 1u : 0u);
+    const uint64_t ps = a + (uint64_t(s.n - 1) << plog), E = a + L;
     s.rows_last = uint32_t(((E + kRowBytes - 1) >> 7) - (ps >> 7));
     s.c_int = s.rows_full + kSortFold;
     s.cost = uint64_t(s.n - 1) * s.c_int + s.rows_last + kSortFold;
@@ -1904,7 +1905,7 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     uint64_t* __restrict__ blk_cost, uint32_t* __restrict__ ctrl, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables)
+    const uint32_t* __restrict__ tables, uint32_t plog)
 {
     static_assert(kSortPer == 1, "one record per thread and cost block");
     constexpr uint32_t X = 1;
@@ -1935,7 +1936,7 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
             }
             else
             {
-                const SortCost sc = sort_cost(uint64_t(p), L);
+                const SortCost sc = sort_cost(uint64_t(p), L, plog);
                 c = sc.cost;
                 if (sc.n > 1) out[r] = ~0u;  // the pieces XOR their parts in
             }
@@ -2093,7 +2094,7 @@ __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ bl
 // records per thread), both at once.  Result in bound[2 h], bound[2 h + 1].
 __device__ __forceinline__ void sort_resolve(const uint8_t* base, const uint64_t* off,
                                              const uint32_t* len, uint64_t count, uint32_t nb,
-                                             SortShared& S)
+                                             SortShared& S, uint32_t plog)
 {
     const uint32_t h = threadIdx.x >> 9, t = threadIdx.x & 511u;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -2105,7 +2106,8 @@ __device__ __forceinline__ void sort_resolve(const uint8_t* base, const uint64_t
     for (uint32_t q = 0; q < 2; ++q)
     {
         sc[q] = SortCost{0, 0, 0, 0, 0};
-        if (j < nb && r0 + q < count) sc[q] = sort_cost(uint64_t(base) + off[r0 + q], len[r0 + q]);
+        if (j < nb && r0 + q < count)
+            sc[q] = sort_cost(uint64_t(base) + off[r0 + q], len[r0 + q], plog);
         mine += sc[q].cost;
     }
     const uint64_t x = wave_incl_scan64(mine);
@@ -2230,9 +2232,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     const uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2)
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog)
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
+    const uint64_t piece = uint64_t(1) << plog;
+    const uint32_t rows_max = uint32_t(piece / kRowBytes) + 1;  // rows of a full piece, unaligned
     const uint32_t lane = threadIdx.x & 63u;
     if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = 0;
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
@@ -2243,7 +2247,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
     // (2) Exact (record, piece) boundaries of this workgroup's items.
-    sort_resolve(base, off, len, count, nb, S);
+    sort_resolve(base, off, len, count, nb, S, plog);
 
     // (3) Bin the items by row count, largest first.  Whole records and the
     // last pieces of split records go to this workgroup's slots of the
@@ -2266,7 +2270,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     auto info = [&](uint64_t r, uint64_t a, uint32_t L) {
         RecInfo f;
-        f.s = sort_cost(a, L);  // L = 0 past rend: no items
+        f.s = sort_cost(a, L, plog);  // L = 0 past rend: no items
         f.klo = r == rlo ? klo0 : 0u;
         const uint32_t khi = r == rhi ? khi0 : f.s.n;
         const uint32_t lim = f.s.n ? f.s.n - 1 : 0u;  // pieces before the last
@@ -2277,7 +2281,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // one returning atomic per full-piece run and per wave leader of a row
     // count; returns (full rank or cursor, last-piece rank or cursor)
     auto take = [&](const RecInfo& f, uint32_t& rf, uint32_t& rl) {
-        rf = f.nf ? atomicAdd(&S.fbins[f.s.rows_full == kSortRows ? 0 : 1], f.nf) : 0u;
+        rf = f.nf ? atomicAdd(&S.fbins[f.s.rows_full == rows_max ? 0 : 1], f.nf) : 0u;
         const uint32_t key = kSortRows - f.s.rows_last;
         const uint64_t eq = match_key10(key, f.last);
         const uint32_t rank = uint32_t(__builtin_popcountll(eq & ((uint64_t(1) << lane) - 1)));
@@ -2287,8 +2291,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         rl = b0 + rank;
     };
     auto desc = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t k) {
-        const uint64_t ps = a + uint64_t(k) * kSortPiece;
-        const uint32_t pl = uint32_t(min<uint64_t>(kSortPiece, a + L - ps));
+        const uint64_t ps = a + (uint64_t(k) << plog);
+        const uint32_t pl = uint32_t(min<uint64_t>(piece, a + L - ps));
         return make_uint4(uint32_t(ps), uint32_t(ps >> 32), pl,
                           uint32_t(r) | (f.s.n > 1 ? kSortMulti : 0u) | (k == 0 ? kSortFirst : 0u));
     };
@@ -2392,7 +2396,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                     if (r < rend)
                     {
                         const RecInfo f = info(r, ha[c][u], hL[c][u]);
-                        const uint32_t fpos = (f.s.rows_full == kSortRows ? 0u : f513) + hf[c][u];
+                        const uint32_t fpos = (f.s.rows_full == rows_max ? 0u : f513) + hf[c][u];
                         place(r, ha[c][u], hL[c][u], f, fpos,
                               f.last ? S.bins[kSortRows - f.s.rows_last] + hl[c][u] : 0u);
                     }
@@ -2689,16 +2693,16 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     const uint32_t nb = sorted_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
     hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
-                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables);
+                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
     hipLaunchKernelGGL(crc32c_sorted_kernel, dim3(grid), dim3(kBlock), kLdsSorted, stream, b,
                        offsets, lengths, inits, count, ws.blk_cost, nb, ws.ctrl, ws.items,
-                       ws.item_cap, ws.wr, out, tables, pow2);
+                       ws.item_cap, ws.wr, out, tables, pow2, ws.plog);
     return hipGetLastError();
 }
 
-uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes)
+uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog)
 {
-    return count + total_bytes / kSortPiece + 1;
+    return count + (total_bytes >> plog) + 1;
 }
 
 // Allow the 152 KiB dynamic LDS image on the two persistent kernels.

@@ -499,7 +499,8 @@ const uint8_t* mapped_device_ptr(const void* p)
 // into pageable memory reach the kernel, which would then read past the
 // mapping.  Both ends must be mapped, at device addresses the
 // same distance apart; when the runtime reports the device allocation's
-// range, the span's end must lie inside it too.
+// range, the span must lie inside it too (tools/zc_probe.py:
+// profiles/r04_zero_copy_pointer_probe.txt).
 const uint8_t* mapped_span_device_ptr(const uint8_t* p, uint64_t n)
 {
     const uint8_t* d0 = mapped_device_ptr(p);
@@ -508,7 +509,9 @@ const uint8_t* mapped_span_device_ptr(const uint8_t* p, uint64_t n)
     if (!d1 || d1 < d0 || uint64_t(d1 - d0) != n - 1) return nullptr;
     hipDeviceptr_t pbase = nullptr;
     size_t psize = 0;
-    if (hipMemGetAddressRange(&pbase, &psize, const_cast<uint8_t*>(d0)) == hipSuccess)
+    // (for hipHostRegister'ed memory ROCm 7.2 reports the size with a null
+    // base: then the two-point check stands alone)
+    if (hipMemGetAddressRange(&pbase, &psize, const_cast<uint8_t*>(d0)) == hipSuccess && pbase)
     {
         const uint8_t* b = static_cast<const uint8_t*>(pbase);
         if (d0 < b || uint64_t(d1 - b) >= psize) return nullptr;
@@ -534,9 +537,13 @@ uint32_t apply_zeros(const DeviceState* d, uint32_t s, uint64_t n)
 }
 
 // MI_CRC32C_VARPATH=pieces|sorted: the variable-length path for batches the
-// direct kernel does not take.  Default: the sorted path when the batch's
-// total bytes are known and at least kSortedMinBytes, else the piece path.
-// "sorted" takes it for every size with a known total (tests), "pieces" never.
+// direct kernel does not take.  Default (round 4): the sorted path whenever
+// the batch's total bytes are known, its pieces sized by sorted_piece_log2
+// (with 4-16 KiB pieces it beats the piece path at every size: 1 MiB 0.029
+// against 0.056 ms, 64 MiB 0.038 against 0.138, 512 MiB 0.119 against
+// 0.186); the piece path when the total is not given (its plan reads the
+// item count back).  "pieces" forces the piece path (tests), "sorted" is the
+// default made explicit.
 int varpath_forced()
 {
     // read per batch (not cached) so that a test can switch paths in-process
@@ -549,11 +556,33 @@ int varpath_forced()
 // The stamp area of the last sorted batch (MI_SORT_STAMP measurement builds).
 uint64_t* last_sorted_stamps = nullptr;
 
+// Piece size of the sorted path by batch size.  A team hashes one item (a
+// whole record, or a piece of a longer one) serially, one row in flight, so
+// the largest item bounds a small batch: 64 KiB pieces made every batch of
+// 1-512 MiB take 0.13-0.19 ms.  Smaller pieces cost a fold and a combine
+// each, which the full configs[2] batch pays for.  Measured (tools/mid_probe.py,
+// configs[2] records cut to size, ms per device batch; profiles/r04_sorted_piece_sweep.txt):
+//   batch     1 MiB  4 MiB  16 MiB  64 MiB  256 MiB  512 MiB  1 GiB  2 GiB  4.9 GB
+//   4 KiB     .029   .033   .034    .038    .077     .131     .237   .449   .990
+//   8 KiB     .037   .042   .042    .046    .074     .122     .213   .402   .898
+//   16 KiB    .054   .056   .062    .062    .077     .119     .209   .378   .853
+//   64 KiB    .135   .158   .155    .166    .171     .187     .250   .392   .813
+uint32_t sorted_piece_log2(uint64_t total_bytes)
+{
+    if (total_bytes < (uint64_t(192) << 20)) return 12;
+    if (total_bytes < (uint64_t(384) << 20)) return 13;
+    if (total_bytes < (uint64_t(3) << 30)) return 14;
+    return kSortPieceLog2;
+}
+
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
 int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
 {
-    const uint64_t cap = sorted_item_cap(count, total_bytes);
+    uint32_t plog = sorted_piece_log2(total_bytes);
+    if (const char* e = std::getenv("MI_CRC32C_SORT_PIECE_LOG2"))
+        plog = uint32_t(std::max(9, std::min(int(kSortPieceLog2), std::atoi(e))));
+    const uint64_t cap = sorted_item_cap(count, total_bytes, plog);
     int st;
     // + a stamp area for MI_SORT_STAMP measurement builds (8 words per wave);
     // ctrl: 64 words, then one 256-B slot per workgroup (MI_SORT_GGRAB builds)
@@ -565,7 +594,7 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     uint8_t* const ib = c->srt_items.as<uint8_t>();
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
-                       reinterpret_cast<uint32_t*>(ib + cap * 16 + 65536 * 64)};
+                       reinterpret_cast<uint32_t*>(ib + cap * 16 + 65536 * 64), plog};
     last_sorted_stamps = reinterpret_cast<uint64_t*>(ib + cap * 16);
     // MI_CRC32C_SORTED_GRID=k: k workgroups instead of one per CU (tests: one
     // workgroup puts every item of a small batch into one sorted list)
@@ -628,8 +657,7 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
                               d->d_pow2, d->cus, c->stream, nullptr, direct_lite_mode()));
         return MI_CRC32C_OK;
     }
-    if (total_bytes && count < kSortedMaxCount && varpath_forced() != 1 &&
-        (total_bytes >= kSortedMinBytes || varpath_forced() == 2))
+    if (total_bytes && count < kSortedMaxCount && varpath_forced() != 1)
         return run_sorted(d, c, base, off, len, inits, count, total_bytes, out);
     const uint32_t nb = var_plan_blocks(count);
     int st;

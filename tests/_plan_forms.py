@@ -2,7 +2,9 @@
 as a subprocess with MI_CRC32C_PLAN_SCAN=1): the scatter deriving its bin
 bases from the per-block counts, or the separate scan pass that plans of more
 than 16M records take.  Long records (> 64 interior pieces) are folded by the
-finalize's block-wide pass."""
+finalize's block-wide pass.  The piece path is forced (MI_CRC32C_VARPATH=
+pieces): with the total known the engine takes the sorted path by default.
+"""
 import os
 import sys
 
@@ -13,6 +15,22 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
 
+def _pieces(fn):
+    """Run fn with the piece path forced, restoring the environment after."""
+    def wrapped(*a, **k):
+        old = os.environ.get("MI_CRC32C_VARPATH")
+        os.environ["MI_CRC32C_VARPATH"] = "pieces"
+        try:
+            return fn(*a, **k)
+        finally:
+            if old is None:
+                os.environ.pop("MI_CRC32C_VARPATH", None)
+            else:
+                os.environ["MI_CRC32C_VARPATH"] = old
+    return wrapped
+
+
+@_pieces
 def many_records(engine, oracle):
     """6.5M short records, a few multi-chunk ones: 1,587 plan blocks (the
     scan pass, when forced, runs over several LDS tiles)."""
@@ -37,6 +55,7 @@ def many_records(engine, oracle):
     assert np.array_equal(got, oracle.batch(host, offsets, lengths)), "many records"
 
 
+@_pieces
 def long_records(engine, oracle):
     """2,000 records, 70 of them 264 KiB - 3 MiB (65 - 770 interior pieces),
     at unaligned starts, with and without inits."""

@@ -93,21 +93,26 @@ def test_fuzz_round(engine, oracle, round_):
         engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini, total_bytes=hint)
         assert np.array_equal(d_out.download(np.uint32, count), want), ("device", hint)
 
-    # the sorted path (forced here; the engine takes it by itself from 512 MiB),
-    # one workgroup per CU or a few workgroups (shares cut inside records)
+    # the sorted path again (the hinted call above took it with its batch-sized
+    # piece), one workgroup per CU or a few workgroups (shares cut inside
+    # records), at a random piece size (512 B - 64 KiB)
     grid = [None, "1", "2", "5", "64"][int(rng.integers(0, 5))]
+    plog = [None, "9", "10", "12", "13", "14", "16"][int(rng.integers(0, 7))]
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
     if grid:
         os.environ["MI_CRC32C_SORTED_GRID"] = grid
+    if plog:
+        os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = plog
     try:
         before = engine.stats()["sorted_batches"]
         engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini,
                             total_bytes=max(int(lengths.sum(dtype=np.uint64)), 1))
-        assert np.array_equal(d_out.download(np.uint32, count), want), ("sorted", grid)
+        assert np.array_equal(d_out.download(np.uint32, count), want), ("sorted", grid, plog)
         assert engine.stats()["sorted_batches"] == before + 1
     finally:
         os.environ.pop("MI_CRC32C_VARPATH", None)
         os.environ.pop("MI_CRC32C_SORTED_GRID", None)
+        os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
 
     # single buffers: one record on the host and on the device
     i = int(rng.integers(0, count))

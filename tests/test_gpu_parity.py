@@ -60,8 +60,16 @@ def test_fixed_shapes(engine, oracle, length, stride):
 
 
 # Host batches of short records take the one-launch direct kernel; planned=True
+# skips it (the sorted path, the default with the total known), "pieces"
 # forces plan -> chunks -> finalize on the same inputs.
-PATHS = pytest.mark.parametrize("planned", [False, True], ids=["direct", "planned"])
+PATHS = pytest.mark.parametrize("planned", [False, True, "pieces"],
+                                ids=["direct", "sorted", "pieces"])
+
+
+@pytest.fixture(autouse=True)
+def _force_pieces(request, monkeypatch):
+    if "planned" in request.fixturenames and request.getfixturevalue("planned") == "pieces":
+        monkeypatch.setenv("MI_CRC32C_VARPATH", "pieces")
 
 
 @PATHS
@@ -323,11 +331,12 @@ def test_device_single_buffer_sweep(engine, oracle):
 
 
 @pytest.mark.parametrize("shape", ["only_4_group", "only_short", "mixed_tiny"])
-def test_var_chunk_roles(engine, oracle, shape):
+def test_var_chunk_roles(engine, oracle, shape, monkeypatch):
     """The chunk launch gives all 16 waves to one role when the other has no
     pieces: batches of 4 KiB-aligned 4 KiB records (only 4-group pieces),
     of records under 1 KiB (only 1- and 2-group pieces), and a tiny mixed
-    batch whose grid is smaller than the chip."""
+    batch whose grid is smaller than the chip.  (Piece path forced.)"""
+    monkeypatch.setenv("MI_CRC32C_VARPATH", "pieces")
     rng = np.random.default_rng(31)
     if shape == "only_4_group":
         count = 3000

@@ -1,10 +1,12 @@
 """GPU parity of the sorted variable-length path:
 one team per whole record, records binned by row count inside each
-workgroup's cost-balanced share, split records (> 64 KiB) XORed together
-from 64 KiB pieces.  Forced here with MI_CRC32C_VARPATH=sorted (the engine
-takes it by itself for batches of >= 512 MiB); every result is compared with
-the CPU oracle, bit-exact, and the path is checked to have run
-(mi_crc32c_stats().sorted_batches).
+workgroup's cost-balanced share, split records XORed together from their
+pieces.  The piece is sized by the batch (4 KiB below 192 MiB ... 64 KiB from
+3 GiB, engine.hip sorted_piece_log2); every test runs with the size's own
+piece ("auto") and with 64 KiB pieces forced (MI_CRC32C_SORT_PIECE_LOG2=16,
+the configs[2] piece).  MI_CRC32C_VARPATH=sorted makes the default explicit;
+every result is compared with the CPU oracle, bit-exact, and the path is
+checked to have run (mi_crc32c_stats().sorted_batches).
 """
 import os
 
@@ -14,12 +16,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def sorted_path(engine):
+@pytest.fixture(params=["auto", "16"], ids=["piece_auto", "piece_64k"])
+def sorted_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
+    if request.param != "auto":
+        os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = request.param
     before = engine.stats()["sorted_batches"]
     yield lambda: engine.stats()["sorted_batches"] - before
+    os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
     if old is None:
         del os.environ["MI_CRC32C_VARPATH"]
     else:
@@ -256,23 +261,41 @@ def test_sorted_matches_piece_path(engine, oracle):
     assert np.array_equal(b, oracle.batch(buf, offsets, lengths))
 
 
-def test_sorted_default_for_large_batches(engine, oracle):
-    """Without the knob, a batch of >= 512 MiB takes the sorted path and one
-    just below it the piece path (kSortedMinBytes, the measured crossover)."""
-    rng = np.random.default_rng(19)
-    count = 160_000
+def _device_run_no_hint(engine, buf, offsets, lengths):
+    count = lengths.size
+    data = engine.DeviceBuffer(max(buf.size, 16))
+    data.upload(buf)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    engine.device_batch(data, d_off, d_len, count, d_out)
+    got = d_out.download(np.uint32, count)
+    for b in (data, d_off, d_len, d_out):
+        b.free()
+    return got
+
+
+@pytest.mark.parametrize("mib", [1, 64, 300, 400])
+def test_sorted_default_with_known_total(engine, oracle, mib):
+    """Without the knob, a device batch whose total is given takes the sorted
+    path at every size (round 4: with batch-sized pieces it is the faster
+    path from 1 MiB up); without the total, the piece path (its plan reads
+    the item count back)."""
+    rng = np.random.default_rng(19 + mib)
+    count = (mib << 20) // 3400 + 1
     lengths = rng.integers(3300, 3500, count).astype(np.uint32)
-    assert int(lengths.sum(dtype=np.uint64)) >= 512 << 20
+    lengths[rng.integers(0, count, 8)] = rng.integers(20_000, 200_000, 8)
     offsets, end = _packed(rng, lengths)
     buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
     want = oracle.batch(buf, offsets, lengths)
     before = engine.stats()["sorted_batches"]
     assert np.array_equal(_device_run(engine, buf, offsets, lengths), want)
     assert engine.stats()["sorted_batches"] == before + 1
-    k = int(np.searchsorted(np.cumsum(lengths, dtype=np.uint64), np.uint64(512 << 20)))
-    before = engine.stats()["sorted_batches"]
-    assert np.array_equal(_device_run(engine, buf, offsets[:k], lengths[:k]), want[:k])
-    assert engine.stats()["sorted_batches"] == before
+    if mib <= 64:
+        before = engine.stats()["sorted_batches"]
+        assert np.array_equal(_device_run_no_hint(engine, buf, offsets, lengths), want)
+        assert engine.stats()["sorted_batches"] == before
 
 
 @pytest.mark.parametrize("seed", range(10))

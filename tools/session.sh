@@ -12,7 +12,7 @@ cd "$ROOT" || exit 9
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
   echo "== $name"
-  timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" || { echo "FAILED $name rc=$?"; tail -30 "$OUT/$name.out" "$OUT/$name.err"; exit 1; }
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" || { echo "FAILED $name rc=$?"; tail -n 30 "$OUT/$name.out" "$OUT/$name.err"; exit 1; }
   tail -3 "$OUT/$name.out"
 }
 while [ $# -gt 0 ]; do
@@ -61,6 +61,22 @@ while [ $# -gt 0 ]; do
     sorted) run pytest_sorted 600 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread ;;
     ab) AB_ROUNDS=${AB_ROUNDS:-3} run ab 900 python3 -u tools/ab.py --zipf "$@"; break ;;
     abfixed) AB_ROUNDS=${AB_ROUNDS:-3} run abfixed 900 python3 -u tools/ab.py "$@"; break ;;
+    # kernel stats of the shipped build: the headline and configs[2] (sorted path)
+    profhead) for cfg in fixed4k zipf; do
+               (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$cfg" -o k -- python3 "$ROOT/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu --no-pmc --no-legs --sustain-seconds 0 > "$OUT/prof_$cfg.log" 2>&1) || { tail -20 "$OUT/prof_$cfg.log"; exit 1; }
+               find "$OUT/prof_$cfg" -name '*kernel_stats.csv' -exec cp {} "$OUT/${cfg}_kernel_stats.csv" \;
+               tail -1 "$OUT/prof_$cfg.log" > "$OUT/${cfg}_bench_under_prof.json"
+               rm -rf "$OUT/prof_$cfg"; head -6 "$OUT/${cfg}_kernel_stats.csv"
+             done ;;
+    zc) run zc_probe 120 python3 tools/zc_probe.py ;;
+    mid) for pth in pieces sorted; do run mid_$pth 300 python3 -u tools/mid_probe.py --path $pth --mib ${MID_MIB:-1,4,16,64,256} --reps 200 || exit 1; done ;;
+    midprof) for pth in pieces sorted; do
+               (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/midprof_$pth" -o k -- python3 "$ROOT/tools/mid_probe.py" --path $pth --mib ${MID_MIB:-64} --reps 50 > "$OUT/midprof_$pth.log" 2>&1) || { tail -20 "$OUT/midprof_$pth.log"; exit 1; }
+               find "$OUT/midprof_$pth" -name '*kernel_stats.csv' -exec cp {} "$OUT/midprof_${pth}_kernel_stats.csv" \;
+               find "$OUT/midprof_$pth" -name '*kernel_trace.csv' -exec python3 tools/trace_summary.py {} \; > "$OUT/midprof_${pth}_trace.txt" 2>&1
+               rm -rf "$OUT/midprof_$pth"; cat "$OUT/midprof_${pth}_trace.txt"
+             done ;;
+    piecesweep) for pl in ${PLOGS:-16 14 13 12 11}; do MI_CRC32C_SORT_PIECE_LOG2=$pl run mid_sorted_p$pl 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-16,64,256} --reps 100 || exit 1; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
