@@ -440,7 +440,10 @@ def run_dlog(args, compact: bool = False) -> dict:
     def per_flush(x):
         f = max(x["flushes"], 1)
         return {"flushes": x["flushes"], "frame_bytes_per_flush": round(x["frame_bytes"] / f),
-                "us_per_flush": {k: round(v / f * 1e6, 2) for k, v in x["flush_s"].items()}}
+                "us_per_flush": {k: round(v / f * 1e6, 2) for k, v in x["flush_s"].items()},
+                # the flush thread's checksum seconds over the whole run
+                "checksum_s": round(x["flush_s"]["batch_crc"], 4),
+                "run_s": round(x["durable_s"], 4)}
     best = median(runs["gpu"])
     pf = per_flush(best)
     # the per-flush bound of the GPU batch: the round trip of a one-frame batch

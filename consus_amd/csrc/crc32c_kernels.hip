@@ -1848,8 +1848,8 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
 constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
 constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 1;  // rows of the largest item (513)
 constexpr uint32_t kSortBins = kSortRows;                         // bin = kSortRows - rows
-// rows per ring of the sorted kernel (4 measured slower: profiles/r03_sorted_wave_roles_ab.txt)
-constexpr int kSortRing = 2;
+// rows per ring of the sorted kernel: a template parameter (2 for 64 KiB pieces;
+// 4 measured slower there: profiles/r03_sorted_wave_roles_ab.txt)
 // XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
 // and in every timeline measured (round 2's stamped builds, 5 GPU sessions,
 // profiles/r02_sorted_stamps_timeline.txt)
@@ -2227,6 +2227,7 @@ __device__ __forceinline__ uint32_t zshift48(const uint32_t* __restrict__ pow2, 
     return v;
 }
 
+template <int RB>
 __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
@@ -2242,12 +2243,21 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     stage_tables(tables);  // ends with a barrier
+#if defined(MI_SORT_STOP)
+    if (MI_SORT_STOP == 1) return;
+#endif
 
     // (1) Wave 0: the two targets and the cost blocks holding them.
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
+#if defined(MI_SORT_STOP)
+    if (MI_SORT_STOP == 2) return;
+#endif
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S, plog);
+#if defined(MI_SORT_STOP)
+    if (MI_SORT_STOP == 3) return;
+#endif
 
     // (3) Bin the items by row count, largest first.  Whole records and the
     // last pieces of split records go to this workgroup's slots of the
@@ -2381,6 +2391,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         }
     }
     __syncthreads();
+#if defined(MI_SORT_STOP)
+    if (MI_SORT_STOP == 4) return;
+#endif
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     if (n_items)
     {
@@ -2407,6 +2420,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     __syncthreads();
     if (n_items == 0) return;
+#if defined(MI_SORT_STOP)
+    if (MI_SORT_STOP == 5) return;
+#endif
 
     // (4) Groups of 8 items, largest first, one LDS grab per group.
     const uint32_t n_groups = (n_items + 7) / 8;
@@ -2479,7 +2495,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             rmax = t <= tlast ? max(rmax, x) : rmax;
             rmin = t <= tlast ? min(rmin, x) : rmin;
         }
-        s.n = (rmax + kSortRing - 1) & ~(kSortRing - 1);
+        s.n = (rmax + RB - 1) & ~(RB - 1);
         s.fmin = s.n - rmax;
         s.fedge = s.n - rmin + 1;
         s.fast = tlast == 7 ? s.fedge + 1 : s.n;
@@ -2508,8 +2524,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
     // flight per wave while another folds (measured on the headline batch:
     // one row ahead costs < 1 % against three; here it keeps the padding to
-    // half a row per group).
-    constexpr int RB = kSortRing;
+    // half a row per group).  RB = 4 is instantiated for small batches
+    // (pieces below 64 KiB), where a wave has only a group or two of up to 33
+    // rows, so the rows in flight per wave, not the HBM, may bound it (round 4,
+    // profiles/r04_sorted_ring_sweep.txt).  RB = 8 needs 129 VGPRs (spills).
     uint4 b[RB];
 #pragma unroll
     for (int j = 0; j < RB - 1; ++j) b[j] = load16(row_ptr(cur0, j, false));
@@ -2633,6 +2651,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
+#if defined(MI_SORT_STOP)
+    if (MI_SORT_STOP == 6) return;
+#endif
     // Finish pass, in record order: a whole record's fold value (wr at its
     // slot) is Z_m(raw) of its bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).
     // (Split records were finished by their pieces' XORs.)
@@ -2694,9 +2715,10 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     const uint8_t* b = static_cast<const uint8_t*>(base);
     hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
-    hipLaunchKernelGGL(crc32c_sorted_kernel, dim3(grid), dim3(kBlock), kLdsSorted, stream, b,
-                       offsets, lengths, inits, count, ws.blk_cost, nb, ws.ctrl, ws.items,
-                       ws.item_cap, ws.wr, out, tables, pow2, ws.plog);
+    auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
+                       count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
+                       pow2, ws.plog);
     return hipGetLastError();
 }
 
@@ -2730,9 +2752,11 @@ hipError_t configure_kernels()
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_sorted_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSorted);
+    const void* ks[] = {reinterpret_cast<const void*>(&crc32c_sorted_kernel<2>),
+                        reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>)};
+    for (const void* f : ks)
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSorted);
     return e;
 }
 

@@ -567,12 +567,28 @@ uint64_t* last_sorted_stamps = nullptr;
 //   8 KiB     .037   .042   .042    .046    .074     .122     .213   .402   .898
 //   16 KiB    .054   .056   .062    .062    .077     .119     .209   .378   .853
 //   64 KiB    .135   .158   .155    .166    .171     .187     .250   .392   .813
+constexpr int kSortRingSmall = 2;
+
 uint32_t sorted_piece_log2(uint64_t total_bytes)
 {
     if (total_bytes < (uint64_t(192) << 20)) return 12;
     if (total_bytes < (uint64_t(384) << 20)) return 13;
     if (total_bytes < (uint64_t(3) << 30)) return 14;
     return kSortPieceLog2;
+}
+
+// Rows in flight per wave in the sorted kernel's hash loop: 64 KiB pieces
+// (the full configs[2] batch, HBM-bound) take the 2-row ring, smaller pieces
+// (batches below 3 GiB, where a wave has a group or two) a deeper one.
+// MI_CRC32C_SORT_RING=2|4 overrides (A/B, tests).
+int sorted_ring(uint32_t plog)
+{
+    if (const char* e = std::getenv("MI_CRC32C_SORT_RING"))
+    {
+        const int r = std::atoi(e);
+        if (r == 2 || r == 4) return r;
+    }
+    return plog < kSortPieceLog2 ? kSortRingSmall : 2;
 }
 
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
@@ -594,7 +610,8 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     uint8_t* const ib = c->srt_items.as<uint8_t>();
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
-                       reinterpret_cast<uint32_t*>(ib + cap * 16 + 65536 * 64), plog};
+                       reinterpret_cast<uint32_t*>(ib + cap * 16 + 65536 * 64), plog,
+                       sorted_ring(plog)};
     last_sorted_stamps = reinterpret_cast<uint64_t*>(ib + cap * 16);
     // MI_CRC32C_SORTED_GRID=k: k workgroups instead of one per CU (tests: one
     // workgroup puts every item of a small batch into one sorted list)

@@ -21,6 +21,8 @@ def arg(name, default):
 
 
 SIZES = [int(x) for x in arg("--mib", "1,4,16,64,256").split(",")]
+if "--lib" in sys.argv:
+    E.LIB_PATH = os.path.abspath(arg("--lib", ""))
 REPS = int(arg("--reps", "200"))
 PATH = arg("--path", "")
 if PATH:
@@ -44,6 +46,7 @@ def warm(seconds=0.3):
         E.sync()
 
 
+TAG = os.path.basename(arg("--lib", "")) or (PATH or "engine")
 print(f"path={PATH or 'engine'}  {'MiB':>5} {'records':>8} {'bytes':>11}  ms/batch   GB/s   check",
       flush=True)
 for mib in SIZES:
@@ -66,5 +69,5 @@ for mib in SIZES:
     for _ in range(REPS):
         E.device_batch(data, d_off, d_len, n, out, total_bytes=total, asynchronous=True)
     ms = E.timer_stop() / REPS
-    print(f"path={PATH or 'engine'}  {mib:5d} {n:8d} {total:11d}  {ms:8.4f} {total / ms / 1e6:7.1f}   "
+    print(f"{TAG}  {mib:5d} {n:8d} {total:11d}  {ms:8.4f} {total / ms / 1e6:7.1f}   "
           f"{'OK' if ok else 'MISMATCH'}", flush=True)

@@ -16,10 +16,11 @@ E.init(0)
 data = E.DeviceBuffer(count * L)
 out = E.DeviceBuffer(count * 4)
 data.fill_splitmix64(0xC0DE)
-for _ in range(3):
-    E.device_batch_fixed(data, L, L, count, out)
+for _ in range(int(os.environ.get("PERF_WARM", "3"))):
+    E.device_batch_fixed(data, L, L, count, out, asynchronous=True)
+E.sync()
 times = []
-for _ in range(20):
+for _ in range(int(os.environ.get("PERF_N", "20"))):
     E.timer_start()
     E.device_batch_fixed(data, L, L, count, out, asynchronous=True)
     times.append(E.timer_stop())

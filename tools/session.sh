@@ -70,13 +70,15 @@ while [ $# -gt 0 ]; do
              done ;;
     zc) run zc_probe 120 python3 tools/zc_probe.py ;;
     mid) for pth in pieces sorted; do run mid_$pth 300 python3 -u tools/mid_probe.py --path $pth --mib ${MID_MIB:-1,4,16,64,256} --reps 200 || exit 1; done ;;
-    midprof) for pth in pieces sorted; do
+    midprof) for pth in ${MID_PATHS:-pieces sorted}; do
                (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/midprof_$pth" -o k -- python3 "$ROOT/tools/mid_probe.py" --path $pth --mib ${MID_MIB:-64} --reps 50 > "$OUT/midprof_$pth.log" 2>&1) || { tail -20 "$OUT/midprof_$pth.log"; exit 1; }
-               find "$OUT/midprof_$pth" -name '*kernel_stats.csv' -exec cp {} "$OUT/midprof_${pth}_kernel_stats.csv" \;
-               find "$OUT/midprof_$pth" -name '*kernel_trace.csv' -exec python3 tools/trace_summary.py {} \; > "$OUT/midprof_${pth}_trace.txt" 2>&1
+               find "$OUT/midprof_$pth" -name '*kernel_trace.csv' -exec python3 "$ROOT/tools/kernel_gaps.py" {} 300 \; > "$OUT/midprof_${pth}_trace.txt" 2>&1
                rm -rf "$OUT/midprof_$pth"; cat "$OUT/midprof_${pth}_trace.txt"
              done ;;
     piecesweep) for pl in ${PLOGS:-16 14 13 12 11}; do MI_CRC32C_SORT_PIECE_LOG2=$pl run mid_sorted_p$pl 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-16,64,256} --reps 100 || exit 1; done ;;
+    ringsweep) for rg in ${RINGS:-2 4}; do MI_CRC32C_SORT_RING=$rg run mid_sorted_ring$rg 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,4,16,64,256,512,1024,2048} --reps 100 || exit 1; done ;;
+    stops) for rnd in 1 2; do for v in ${STOPS:-stop1 stop2 stop3 stop4 stop5 stop6 full}; do timeout -k 10 120 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,64,256} --reps 100 --lib tools/ab/libconsus_crc32c_$v.so 2>&1 | grep -v "MiB" || exit 1; done; done | tee "$OUT/stops.out" ;;
+    headab) cp consus_amd/lib/libconsus_crc32c.so tools/ab/libconsus_crc32c_r04.so && PERF_WARM=300 PERF_N=200 AB_ROUNDS=${AB_ROUNDS:-4} run headab 600 python3 -u tools/ab.py tools/ab/libconsus_crc32c_r02.so tools/ab/libconsus_crc32c_r03.so tools/ab/libconsus_crc32c_r04.so && cat "$OUT/headab.out" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
