@@ -567,7 +567,10 @@ uint64_t* last_sorted_stamps = nullptr;
 //   8 KiB     .037   .042   .042    .046    .074     .122     .213   .402   .898
 //   16 KiB    .054   .056   .062    .062    .077     .119     .209   .378   .853
 //   64 KiB    .135   .158   .155    .166    .171     .187     .250   .392   .813
-constexpr int kSortRingSmall = 2;
+// (4 against 2, ms per device batch: 1 MiB .027/.029, 16 MiB .031/.034,
+// 256 MiB .072/.074, 1 GiB .207/.218, 2 GiB .391/.395;
+// profiles/r04_sorted_ring_sweep.txt)
+constexpr int kSortRingSmall = 4;
 
 uint32_t sorted_piece_log2(uint64_t total_bytes)
 {
