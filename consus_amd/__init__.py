@@ -22,6 +22,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libconsus_crc32c.so")
+_DEFAULT_LIB = LIB_PATH
 REPO = os.path.dirname(HERE)
 HEADERS = [os.path.join(REPO, "include", "consus_crc32c.h"),
            os.path.join(REPO, "include", "consus_durable_log.h")]
@@ -132,7 +133,12 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise EngineError(ENODEV, "load", f"{LIB_PATH} missing: run consus_amd.build()")
         L = C.CDLL(LIB_PATH)
+        # an A/B build of an earlier round (tools/ab.py, LIB_PATH pointed
+        # elsewhere) may lack later entry points; the in-tree library may not
+        in_tree = os.path.abspath(LIB_PATH) == os.path.abspath(_DEFAULT_LIB)
         for name, (res, args) in _SIGS.items():
+            if not in_tree and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -2243,21 +2243,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     stage_tables(tables);  // ends with a barrier
-#if defined(MI_SORT_STOP)
-    if (MI_SORT_STOP == 1) return;
-#endif
 
     // (1) Wave 0: the two targets and the cost blocks holding them.
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
-#if defined(MI_SORT_STOP)
-    if (MI_SORT_STOP == 2) return;
-#endif
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S, plog);
-#if defined(MI_SORT_STOP)
-    if (MI_SORT_STOP == 3) return;
-#endif
 
     // (3) Bin the items by row count, largest first.  Whole records and the
     // last pieces of split records go to this workgroup's slots of the
@@ -2391,9 +2382,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         }
     }
     __syncthreads();
-#if defined(MI_SORT_STOP)
-    if (MI_SORT_STOP == 4) return;
-#endif
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     if (n_items)
     {
@@ -2420,9 +2408,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     __syncthreads();
     if (n_items == 0) return;
-#if defined(MI_SORT_STOP)
-    if (MI_SORT_STOP == 5) return;
-#endif
 
     // (4) Groups of 8 items, largest first, one LDS grab per group.
     const uint32_t n_groups = (n_items + 7) / 8;
@@ -2651,9 +2636,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
-#if defined(MI_SORT_STOP)
-    if (MI_SORT_STOP == 6) return;
-#endif
     // Finish pass, in record order: a whole record's fold value (wr at its
     // slot) is Z_m(raw) of its bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).
     // (Split records were finished by their pieces' XORs.)

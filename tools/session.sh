@@ -79,6 +79,7 @@ while [ $# -gt 0 ]; do
     ringsweep) for rg in ${RINGS:-2 4}; do MI_CRC32C_SORT_RING=$rg run mid_sorted_ring$rg 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,4,16,64,256,512,1024,2048} --reps 100 || exit 1; done ;;
     stops) for rnd in 1 2; do for v in ${STOPS:-stop1 stop2 stop3 stop4 stop5 stop6 full}; do timeout -k 10 120 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,64,256} --reps 100 --lib tools/ab/libconsus_crc32c_$v.so 2>&1 | grep -v "MiB" || exit 1; done; done | tee "$OUT/stops.out" ;;
     headab) cp consus_amd/lib/libconsus_crc32c.so tools/ab/libconsus_crc32c_r04.so && PERF_WARM=300 PERF_N=200 AB_ROUNDS=${AB_ROUNDS:-4} run headab 600 python3 -u tools/ab.py tools/ab/libconsus_crc32c_r02.so tools/ab/libconsus_crc32c_r03.so tools/ab/libconsus_crc32c_r04.so && cat "$OUT/headab.out" ;;
+    piece4) for pl in 10 11 12 13; do MI_CRC32C_SORT_RING=4 MI_CRC32C_SORT_PIECE_LOG2=$pl run mid_sorted_r4p$pl 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,16,64,256} --reps 100 || exit 1; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
