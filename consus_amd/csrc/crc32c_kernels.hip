@@ -268,6 +268,20 @@ __device__ __forceinline__ uint4 load16(const uint8_t* p)
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// A record's first and last rows share their 128-B lines with the
+// neighbouring records (packed back to back), which another team reads later;
+// read with the default policy those lines may stay in the MALL for it.
+__device__ __forceinline__ uint4 load16_edge(const uint8_t* p)
+{
+#if defined(MI_EDGE_DEFAULT)
+    typedef const __attribute__((address_space(1))) u32x4_t* gptr;
+    const u32x4_t v = *((gptr)(uintptr_t)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return load16(p);
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // Fixed-stride batches: record i = [base + i*stride, +len), base and stride
 // 16-byte aligned, len a multiple of 16 (other shapes take the variable path).
@@ -1846,7 +1860,8 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
 // No plan/finalize passes over the items: one small launch, then the hash.
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
-constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 1;  // rows of the largest item (513)
+// rows of the largest item: a 64 KiB + 3 B head piece at an unaligned start (514)
+constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 2;
 constexpr uint32_t kSortBins = kSortRows;                         // bin = kSortRows - rows
 // rows per ring of the sorted kernel: a template parameter (2 for 64 KiB pieces;
 // 4 measured slower there: profiles/r03_sorted_wave_roles_ab.txt)
@@ -1872,20 +1887,32 @@ struct SortCost
 {
     uint64_t cost;       // all the record's items
     uint32_t n;          // items (pieces); 0: finished by sorted_cost_kernel (L < 4)
-    uint32_t c_int;      // cost of every piece but the last
+    uint32_t c_int;      // cost of every piece but the last (in cost order: the full pieces)
     uint32_t rows_full;  // rows of every piece but the last
-    uint32_t rows_last;
+    uint32_t rows_last;  // rows of the last piece in cost order: the head
 };
 
+// Pieces are cut from the record's END (round 4): the full pieces are
+// [E - P (j + 1), E - P j), so a piece's part of the record CRC is
+// Z_{P j}(raw(piece)), a shift by popcount(j) table lookups (cut from the
+// start, the shift was E - pe = any length: up to 17 dependent L2 lookup
+// rounds per piece, which small batches of 4 KiB pieces waited for).  The
+// head [a, E - P (n - 1)) takes what is left, at least 4 bytes so that the
+// ~init word stays inside it (a shorter remainder joins the next piece: the
+// head then has up to P + 3 bytes).  In piece order the full pieces come
+// first (piece i < n - 1 is the full piece ending P (n - 2 - i) before E) and
+// the head last, so every piece but the last in that order costs c_int.
 __device__ __forceinline__ SortCost sort_cost(uint64_t a, uint32_t L, uint32_t plog)
 {
     SortCost s{0, 0, 0, 0, 0};
     if (L < 4) return s;
     const uint64_t piece = uint64_t(1) << plog;
     s.n = uint32_t((uint64_t(L) + piece - 1) >> plog);
-    s.rows_full = uint32_t(piece / kRowBytes) + ((a & (kRowBytes - 1)) ? 1u : 0u);
-    const uint64_t ps = a + (uint64_t(s.n - 1) << plog), E = a + L;
-    s.rows_last = uint32_t(((E + kRowBytes - 1) >> 7) - (ps >> 7));
+    if (s.n > 1 && uint64_t(L) - (uint64_t(s.n - 1) << plog) < 4) --s.n;  // head >= 4 bytes
+    const uint64_t E = a + L;
+    s.rows_full = uint32_t(piece / kRowBytes) + ((E & (kRowBytes - 1)) ? 1u : 0u);
+    const uint64_t he = E - (uint64_t(s.n - 1) << plog);  // the head's end
+    s.rows_last = uint32_t(((he + kRowBytes - 1) >> 7) - (a >> 7));
     s.c_int = s.rows_full + kSortFold;
     s.cost = uint64_t(s.n - 1) * s.c_int + s.rows_last + kSortFold;
     return s;
@@ -2291,11 +2318,15 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         b0 = uint32_t(__shfl(int(b0), f.last ? int(__builtin_ctzll(eq)) : int(lane)));
         rl = b0 + rank;
     };
+    // piece k in cost order: k < n - 1 the full piece ending P (n - 2 - k)
+    // before E, k = n - 1 the head (carries the init)
     auto desc = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t k) {
-        const uint64_t ps = a + (uint64_t(k) << plog);
-        const uint32_t pl = uint32_t(min<uint64_t>(piece, a + L - ps));
-        return make_uint4(uint32_t(ps), uint32_t(ps >> 32), pl,
-                          uint32_t(r) | (f.s.n > 1 ? kSortMulti : 0u) | (k == 0 ? kSortFirst : 0u));
+        const uint64_t E = a + L;
+        const bool head = k + 1 == f.s.n;
+        const uint64_t pe = E - (uint64_t(head ? f.s.n - 1 : f.s.n - 2 - k) << plog);
+        const uint64_t ps = head ? a : pe - piece;
+        return make_uint4(uint32_t(ps), uint32_t(ps >> 32), uint32_t(pe - ps),
+                          uint32_t(r) | (f.s.n > 1 ? kSortMulti : 0u) | (head ? kSortFirst : 0u));
     };
     uint4* const fullv = items + count;
     uint4* const lastv = items + rlo;
@@ -2515,8 +2546,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // profiles/r04_sorted_ring_sweep.txt).  RB = 8 needs 129 VGPRs (spills).
     uint4 b[RB];
 #pragma unroll
-    for (int j = 0; j < RB - 1; ++j) b[j] = load16(row_ptr(cur0, j, false));
-    if (RB == 2 && shA.n == 2) b[1] = load16(row_ptr(cur0, 1, false));
+    for (int j = 0; j < RB - 1; ++j) b[j] = load16_edge(row_ptr(cur0, j, false));
+    if (RB == 2 && shA.n == 2) b[1] = load16_edge(row_ptr(cur0, 1, false));
     __builtin_amdgcn_sched_barrier(0);
     // One group: hash `cur` (shape sh) while the next group's view is built
     // into `nxt`.  The loop runs it twice per iteration with the two views
@@ -2572,7 +2603,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 #pragma unroll
             for (int j = 0; j < RB; ++j)
             {
-                b[(j + RB - 1) % RB] = load16(row_ptr(cur, r + j + RB - 1, false));
+                {
+                    const int32_t rr = r + j + RB - 1;
+                    const uint8_t* pp = row_ptr(cur, rr, false);
+                    b[(j + RB - 1) % RB] = rr <= fedge ? load16_edge(pp) : load16(pp);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 gen_row(b[j], r + j);
             }
@@ -2595,12 +2630,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         for (int j = 0; j < RB; ++j)
         {
             if (!(j == 0 && pre))
-                b[(j + RB - 1) % RB] = load16(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
+                b[(j + RB - 1) % RB] = load16_edge(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
             __builtin_amdgcn_sched_barrier(0);
             gen_row(b[j], n - RB + j);
         }
         // the next group's row 1 if it has two rows (b[1] is free now)
-        if (RB == 2 && shn.n == 2) b[1] = load16(row_ptr(nxt, 1, false));
+        if (RB == 2 && shn.n == 2) b[1] = load16_edge(row_ptr(nxt, 1, false));
         const uint32_t W = team_fold(V);
         flush();  // the previous group's split-record pieces
         {

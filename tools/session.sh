@@ -80,6 +80,10 @@ while [ $# -gt 0 ]; do
     stops) for rnd in 1 2; do for v in ${STOPS:-stop1 stop2 stop3 stop4 stop5 stop6 full}; do timeout -k 10 120 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,64,256} --reps 100 --lib tools/ab/libconsus_crc32c_$v.so 2>&1 | grep -v "MiB" || exit 1; done; done | tee "$OUT/stops.out" ;;
     headab) cp consus_amd/lib/libconsus_crc32c.so tools/ab/libconsus_crc32c_r04.so && PERF_WARM=300 PERF_N=200 AB_ROUNDS=${AB_ROUNDS:-4} run headab 600 python3 -u tools/ab.py tools/ab/libconsus_crc32c_r02.so tools/ab/libconsus_crc32c_r03.so tools/ab/libconsus_crc32c_r04.so && cat "$OUT/headab.out" ;;
     piece4) for pl in 10 11 12 13; do MI_CRC32C_SORT_RING=4 MI_CRC32C_SORT_PIECE_LOG2=$pl run mid_sorted_r4p$pl 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,16,64,256} --reps 100 || exit 1; done ;;
+    fetchab) for v in ${FETCH_LIBS:-base edge}; do
+               (cd /tmp && ZIPF_WARM=2 ZIPF_ROUNDS=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$v" -o k -- python3 "$ROOT/tools/zipf_probe.py" "$ROOT/tools/ab/libconsus_crc32c_$v.so" > "$OUT/fetch_$v.log" 2>&1) || { tail -5 "$OUT/fetch_$v.log"; exit 1; }
+               echo "== $v (FETCH_SIZE KB x2 per dispatch, median)"; python3 tools/pmc_summary.py "$OUT/fetch_$v" crc32c_sorted_kernel sorted_cost_kernel; rm -rf "$OUT/fetch_$v"
+             done | tee "$OUT/fetchab.out" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
