@@ -134,7 +134,7 @@ struct SortedWorkspace
     uint64_t item_cap;   // sorted_item_cap(count, total_bytes)
     uint32_t* wr;        // item_cap words: a whole record's fold value, by descriptor slot
     uint32_t plog;       // log2 of the piece records longer than it are cut into (9..16)
-    int ring;            // rows per ring of the hash loop: 2 or 4
+    int ring;            // rows per ring of the hash loop: 2, 4 or 8
 };
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);

@@ -2269,7 +2269,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = 0;
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
+    // small batches finish each whole record right after its fold (below):
+    // Z_{-128} is staged with the tables
+    if (RB >= 4) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     stage_tables(tables);  // ends with a barrier
+    constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
 
     // (1) Wave 0: the two targets and the cost blocks holding them.
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
@@ -2344,7 +2348,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         // a whole record's out[] holds its slot until the finish pass (whose
         // record-order reads and stores are coalesced; the loop's fold value
         // goes to wr[slot], contiguous in list order)
-        if (f.last && f.s.n == 1) out[r] = lpos;
+        if (RB == 2 && f.last && f.s.n == 1) out[r] = lpos;
     };
     uint64_t ha[CH][U];
     uint32_t hL[CH][U], hf[CH][U], hl[CH][U];
@@ -2540,10 +2544,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
     // flight per wave while another folds (measured on the headline batch:
     // one row ahead costs < 1 % against three; here it keeps the padding to
-    // half a row per group).  RB = 4 is instantiated for small batches
-    // (pieces below 64 KiB), where a wave has only a group or two of up to 33
-    // rows, so the rows in flight per wave, not the HBM, may bound it (round 4,
-    // profiles/r04_sorted_ring_sweep.txt).  RB = 8 needs 129 VGPRs (spills).
+    // half a row per group).  RB = 4 and 8 are instantiated for small
+    // batches (pieces below 64 KiB), where a wave has only a group or two of
+    // up to 33 rows, so the rows in flight per wave, not the HBM, bound it
+    // (round 4, profiles/r04_sorted_ring_sweep.txt).  They finish whole
+    // records in the loop (no finish pass), which frees the registers RB = 8
+    // needs (128 VGPRs, no scratch).
     uint4 b[RB];
 #pragma unroll
     for (int j = 0; j < RB - 1; ++j) b[j] = load16_edge(row_ptr(cur0, j, false));
@@ -2643,7 +2649,23 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             // whole records: the fold value by slot, eight consecutive words per
             // group (stores to out[rec] here hit a line per record, scattered:
             // 8-11 us of the configs[2] step, profiles/r03_sorted_late_finish_ab.txt)
-            if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
+            if (RB == 2)
+            {
+                if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
+            }
+            else if (cur.recf != kSortNone && !multi)
+            {
+                // small batches (RB >= 4): a wave has a group or two, so the
+                // finish pass's two dependent global reads per record cost
+                // more than finishing here: crc = ~Z_{-m}(W) from LDS tables
+                const uint32_t m = cur.m & 127u, nn = 128u - m;
+                uint32_t t = zT_n(W, nn & 15u);
+                t = (nn & 16u) ? zT<4>(t) : t;
+                t = (nn & 32u) ? zG(kLdsZ32, t) : t;
+                t = (nn & 64u) ? zG(kLdsZ64, t) : t;
+                t = zG(kLdsZInv, t);
+                if (tl == 0) out[cur.recf & kSortRecMask] = ~(m ? t : W);
+            }
             p_multi = __builtin_amdgcn_ballot_w64(multi) != 0;
             if (p_multi)
             {
@@ -2671,12 +2693,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
+    if (RB >= 4) return;  // whole records were finished in the loop
     // Finish pass, in record order: a whole record's fold value (wr at its
     // slot) is Z_m(raw) of its bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).
     // (Split records were finished by their pieces' XORs.)
     S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     __syncthreads();  // the workgroup's own stores are visible to it past the barrier
-    constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
     // four records per thread per round: every load of the round issued
     // before any is used (the pass is two dependent global round trips and
     // five LDS rounds per record; round 3 A/B: -1 to -2 us against one record
@@ -2732,7 +2754,9 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     const uint8_t* b = static_cast<const uint8_t*>(base);
     hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
                        lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
-    auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
+    auto k = ws.ring == 8   ? crc32c_sorted_kernel<8>
+             : ws.ring == 4 ? crc32c_sorted_kernel<4>
+                            : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
                        pow2, ws.plog);
@@ -2770,7 +2794,8 @@ hipError_t configure_kernels()
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);
     const void* ks[] = {reinterpret_cast<const void*>(&crc32c_sorted_kernel<2>),
-                        reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>)};
+                        reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>),
+                        reinterpret_cast<const void*>(&crc32c_sorted_kernel<8>)};
     for (const void* f : ks)
         if (e == hipSuccess)
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSorted);

@@ -583,13 +583,13 @@ uint32_t sorted_piece_log2(uint64_t total_bytes)
 // Rows in flight per wave in the sorted kernel's hash loop: 64 KiB pieces
 // (the full configs[2] batch, HBM-bound) take the 2-row ring, smaller pieces
 // (batches below 3 GiB, where a wave has a group or two) a deeper one.
-// MI_CRC32C_SORT_RING=2|4 overrides (A/B, tests).
+// MI_CRC32C_SORT_RING=2|4|8 overrides (A/B, tests).
 int sorted_ring(uint32_t plog)
 {
     if (const char* e = std::getenv("MI_CRC32C_SORT_RING"))
     {
         const int r = std::atoi(e);
-        if (r == 2 || r == 4) return r;
+        if (r == 2 || r == 4 || r == 8) return r;
     }
     return plog < kSortPieceLog2 ? kSortRingSmall : 2;
 }

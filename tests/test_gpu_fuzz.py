@@ -98,7 +98,7 @@ def test_fuzz_round(engine, oracle, round_):
     # records), at a random piece size (512 B - 64 KiB)
     grid = [None, "1", "2", "5", "64"][int(rng.integers(0, 5))]
     plog = [None, "9", "10", "12", "13", "14", "16"][int(rng.integers(0, 7))]
-    ring = [None, "2", "4"][int(rng.integers(0, 3))]
+    ring = [None, "2", "4", "8"][int(rng.integers(0, 4))]
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
     if ring:
         os.environ["MI_CRC32C_SORT_RING"] = ring

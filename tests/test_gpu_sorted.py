@@ -3,8 +3,8 @@ one team per whole record, records binned by row count inside each
 workgroup's cost-balanced share, split records XORed together from their
 pieces.  The piece is sized by the batch (4 KiB below 192 MiB ... 64 KiB from
 3 GiB, engine.hip sorted_piece_log2); every test runs with the size's own
-piece ("auto") and with 64 KiB pieces forced (MI_CRC32C_SORT_PIECE_LOG2=16,
-the configs[2] piece).  MI_CRC32C_VARPATH=sorted makes the default explicit;
+piece ("auto", 4-row ring), with the 8-row ring, and with 64 KiB pieces
+forced (MI_CRC32C_SORT_PIECE_LOG2=16, the configs[2] piece, 2-row ring).  MI_CRC32C_VARPATH=sorted makes the default explicit;
 every result is compared with the CPU oracle, bit-exact, and the path is
 checked to have run (mi_crc32c_stats().sorted_batches).
 """
@@ -16,15 +16,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["auto", "16"], ids=["piece_auto", "piece_64k"])
+@pytest.fixture(params=["auto", "auto-ring8", "16"], ids=["piece_auto", "piece_auto_ring8", "piece_64k"])
 def sorted_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
-    if request.param != "auto":
+    if request.param == "auto-ring8":
+        os.environ["MI_CRC32C_SORT_RING"] = "8"
+    elif request.param != "auto":
         os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = request.param
     before = engine.stats()["sorted_batches"]
     yield lambda: engine.stats()["sorted_batches"] - before
     os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
+    os.environ.pop("MI_CRC32C_SORT_RING", None)
     if old is None:
         del os.environ["MI_CRC32C_VARPATH"]
     else:
