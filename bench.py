@@ -453,6 +453,23 @@ def run_dlog(args, compact: bool = False) -> dict:
     bound = pf["empty_batch_us"] + pf["frame_bytes_per_flush"] / 55e3
     pf["batch_crc_bound_us"] = round(bound, 2)
     pf["batch_crc_vs_bound"] = round(pf["us_per_flush"]["batch_crc"] / bound, 3)
+    # the same bound with the host link's rate as measured in the run: the
+    # incremental rate of synchronous pinned-to-device copies between the two
+    # timed sizes that bracket the flush (dlog_bench; MB-scale copies get
+    # ~32 GB/s of the link, not the 55 of 64 MiB transfers)
+    link = sorted((int(k), float(v)) for k, v in best.get("link_us", {}).items())
+    if len(link) >= 2:
+        nb = pf["frame_bytes_per_flush"]
+        i = 1
+        while i < len(link) - 1 and link[i][0] < nb:
+            i += 1
+        (n0, t0), (n1, t1) = link[i - 1], link[i]
+        rate = (n1 - n0) / max(t1 - t0, 1e-3)  # bytes per us
+        pf["link_copy_us"] = {str(k): round(v, 2) for k, v in link}
+        pf["link_rate_gb_s"] = round(rate / 1e3, 1)
+        mbound = pf["empty_batch_us"] + nb / rate
+        pf["batch_crc_bound_measured_link_us"] = round(mbound, 2)
+        pf["batch_crc_vs_measured_link"] = round(pf["us_per_flush"]["batch_crc"] / mbound, 3)
     cpu = None
     if "reference-cpu" in runs:
         rb = median(runs["reference-cpu"])

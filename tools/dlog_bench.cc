@@ -119,6 +119,7 @@ int main(int argc, char** argv)
             entry_bytes += lens[t][k];
         }
 
+    std::vector<std::pair<size_t, double>> g_link;  // (bytes, us) of pinned-to-device copies
     const char* ref_so = getenv("REF_CRC_SO");
     if (ref_so && *ref_so)
     {
@@ -154,6 +155,30 @@ int main(int argc, char** argv)
             empty_us = t[t.size() / 2];
             mi_host_free_pinned(pin);
         }
+        // the host link as a flush sees it: a synchronous copy of n bytes of
+        // pinned memory to the device, median of 40, at flush-like sizes
+        void* hp = nullptr;
+        void* dp = nullptr;
+        const size_t big = size_t(16) << 20;
+        if (mi_host_malloc_pinned(&hp, big) == MI_CRC32C_OK && mi_dev_malloc(&dp, big) == MI_CRC32C_OK)
+        {
+            memset(hp, 3, big);
+            for (size_t n : {size_t(64) << 10, size_t(256) << 10, size_t(1) << 20, size_t(4) << 20,
+                             size_t(16) << 20})
+            {
+                std::vector<double> t;
+                for (int i = 0; i < 45; ++i)
+                {
+                    const double a = now();
+                    mi_memcpy(dp, hp, n, MI_MEMCPY_H2D);
+                    if (i >= 5) t.push_back((now() - a) * 1e6);
+                }
+                std::sort(t.begin(), t.end());
+                g_link.push_back({n, t[t.size() / 2]});
+            }
+        }
+        if (dp) mi_dev_free(dp);
+        if (hp) mi_host_free_pinned(hp);
     }
     consus::durable_log log(seg);
     // watchdog: a stage that takes more than DLOG_STAGE_LIMIT s (default 60)
@@ -314,7 +339,15 @@ int main(int argc, char** argv)
     wd_stop.store(true);
     watchdog.join();
     const uint64_t frame_bytes = entry_bytes + total * 20;
-    printf("{\"engine\": \"%s\", \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
+    std::string link = "{";
+    for (size_t i = 0; i < g_link.size(); ++i)
+    {
+        char b[64];
+        snprintf(b, sizeof b, "%s\"%zu\": %.2f", i ? ", " : "", g_link[i].first, g_link[i].second);
+        link += b;
+    }
+    link += "}";
+    printf("{\"engine\": \"%s\", \"link_us\": %s, \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
            "\"append_s\": %.6f, \"durable_s\": %.6f, \"appends_per_s\": %.1f, "
            "\"frame_GiB_per_s\": %.4f, \"flushes\": %llu, \"frames_flushed\": %llu, "
            "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
@@ -324,7 +357,7 @@ int main(int argc, char** argv)
            "\"patch\": %.1f, \"pwrite\": %.1f, \"fsync\": %.1f}, "
            "\"durable_latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, "
            "\"max_at_s\": %.4f, \"samples\": %zu}}\n",
-           fake ? "none" : g_ref ? "reference-cpu" : "gpu", empty_us, threads,
+           fake ? "none" : g_ref ? "reference-cpu" : "gpu", link.c_str(), empty_us, threads,
            (unsigned long long)total,
            (unsigned long long)entry_bytes,
            (unsigned long long)frame_bytes, t_appended - t0, t_durable - t0,
