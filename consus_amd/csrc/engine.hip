@@ -327,7 +327,7 @@ struct Ctx
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
-    DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
+    DevBuf srt_cost, srt_ctrl, srt_items, srt_acc;  // sorted path (launch_sorted)
     DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
     uint32_t done_seq = 0;
     PinBuf pin_small;                   // plan-size read-back; word kDoneWord: completion word
@@ -408,7 +408,7 @@ struct Ctx
         if (stream) (void)hipStreamSynchronize(stream);
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs, &srt_cost,
-                          &srt_ctrl, &srt_items, &done_ctr})
+                          &srt_ctrl, &srt_items, &srt_acc, &done_ctr})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -553,8 +553,16 @@ int varpath_forced()
     return 0;
 }
 
-// The stamp area of the last sorted batch (MI_SORT_STAMP measurement builds).
-uint64_t* last_sorted_stamps = nullptr;
+// A device buffer of at least `bytes` whose new allocations are zeroed (on the
+// stream, before any later work on it).
+int reserve_zeroed(DevBuf& b, size_t bytes, hipStream_t stream)
+{
+    if (bytes <= b.cap) return MI_CRC32C_OK;
+    int st;
+    if ((st = b.reserve(bytes))) return st;
+    HIP_TRY(hipMemsetAsync(b.p, 0, b.cap, stream));
+    return MI_CRC32C_OK;
+}
 
 // Piece size of the sorted path by batch size.  A team hashes one item (a
 // whole record, or a piece of a longer one) serially, one row in flight, so
@@ -601,26 +609,30 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     uint32_t plog = sorted_piece_log2(total_bytes);
     if (const char* e = std::getenv("MI_CRC32C_SORT_PIECE_LOG2"))
         plog = uint32_t(std::max(9, std::min(int(kSortPieceLog2), std::atoi(e))));
-    const uint64_t cap = sorted_item_cap(count, total_bytes, plog);
-    int st;
-    // + a stamp area for MI_SORT_STAMP measurement builds (8 words per wave);
-    // ctrl: 64 words, then one 256-B slot per workgroup (MI_SORT_GGRAB builds)
-    if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
-        (st = c->srt_ctrl.reserve(4 * (64 + 64 * uint64_t(8 * d->cus)))) ||
-        (st = c->srt_items.reserve(cap * 20 + 65536 * 64)))
-        return st;
-    // descriptors, then the stamp area, then the fold values by slot
-    uint8_t* const ib = c->srt_items.as<uint8_t>();
-    SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
-                       reinterpret_cast<uint4*>(ib), cap,
-                       reinterpret_cast<uint32_t*>(ib + cap * 16 + 65536 * 64), plog,
-                       sorted_ring(plog)};
-    last_sorted_stamps = reinterpret_cast<uint64_t*>(ib + cap * 16);
     // MI_CRC32C_SORTED_GRID=k: k workgroups instead of one per CU (tests: one
     // workgroup puts every item of a small batch into one sorted list)
     int grid = d->cus;
     if (const char* e = std::getenv("MI_CRC32C_SORTED_GRID"))
         grid = std::max(1, std::min(8 * grid, std::atoi(e)));
+    const uint64_t cap = sorted_item_cap(count, total_bytes, plog, grid);
+    // MI_CRC32C_SORT_FUSED=0: small batches launch sorted_cost_kernel too (A/B, tests)
+    const char* fe = std::getenv("MI_CRC32C_SORT_FUSED");
+    const bool fused = sorted_fused(count) && !(fe && !std::strcmp(fe, "0"));
+    int st;
+    // ctrl[1] (overflow flag) and the fused accumulators start zero; the
+    // kernels leave the accumulators zero, the host clears a raised flag
+    if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
+        (st = reserve_zeroed(c->srt_ctrl, 64 * 4, c->stream)) ||
+        (st = c->srt_items.reserve(cap * 20)) ||
+        (fused && (st = reserve_zeroed(c->srt_acc, uint64_t(count) * 8, c->stream))))
+        return st;
+    // descriptors, then the fold values by slot
+    uint8_t* const ib = c->srt_items.as<uint8_t>();
+    SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
+                       reinterpret_cast<uint4*>(ib), cap,
+                       reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
+                       sorted_full_per_wg(count, total_bytes, plog, grid),
+                       fused ? c->srt_acc.as<uint32_t>() : nullptr};
     HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
                           c->stream));
     c->sorted_ctrl = ws.ctrl;
@@ -848,6 +860,8 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         HIP_TRY(hipStreamSynchronize(c->stream));
         const bool overflow = c->sorted_ctrl ? *flag != 0 : *flag > c->plan_cap;
         if (!overflow) return MI_CRC32C_OK;
+        // a fused sorted launch runs no cost kernel to clear the flag
+        if (c->sorted_ctrl) HIP_TRY(hipMemsetAsync(c->sorted_ctrl + 1, 0, 4, c->stream));
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, 0, out))) return st;
         return finish(c, flags);
     }
@@ -1364,10 +1378,6 @@ int mi_memset(void* dev, int value, size_t bytes)
     HIP_TRY(hipStreamSynchronize(c->stream));
     return MI_CRC32C_OK;
 }
-
-// Dev tool (not in the public header): the stamp area of the calling
-// thread's last sorted batch, 8 x u64 per wave, MI_SORT_STAMP builds only.
-void* mi_dev_sorted_stamps(void) { return last_sorted_stamps; }
 
 int mi_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t byte_offset)
 {

@@ -331,3 +331,38 @@ def test_sorted_fuzz_large(engine, oracle, sorted_path, seed):
         os.environ.pop("MI_CRC32C_SORTED_GRID", None)
     assert np.array_equal(got, oracle.batch(buf, offsets, lengths, inits)), grid
     assert sorted_path() == 1
+
+
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused", "cost_kernel"])
+def test_sorted_leading_and_trailing_tiny_records(engine, oracle, sorted_path, fused, monkeypatch):
+    """Records shorter than 4 B at the very start and end of the batch (zero
+    cost: no workgroup's share starts on them), split records between them.
+    A fused launch (no sorted_cost_kernel) finishes them in workgroup 0's and
+    the last workgroup's binning pass; MI_CRC32C_SORT_FUSED=0 launches the
+    cost kernel, which finishes them."""
+    monkeypatch.setenv("MI_CRC32C_SORT_FUSED", fused)
+    rng = np.random.default_rng(61)
+    lengths = np.concatenate([rng.integers(0, 4, 300), rng.integers(4, 20_000, 3000),
+                              [70_000, 9000, 200_000], rng.integers(0, 4, 300)]).astype(np.uint32)
+    offsets, end = _packed(rng, lengths, gap=3, start=7)
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+
+
+def test_sorted_fused_accumulators_clean_across_batches(engine, oracle, sorted_path):
+    """The fused launch combines a split record's pieces through accumulators
+    that the last piece leaves zero: many batches in a row on one stream,
+    split records at varying positions, every result exact."""
+    rng = np.random.default_rng(62)
+    for k in range(12):
+        count = int(rng.integers(50, 3000))
+        lengths = rng.integers(0, 9000, count).astype(np.uint32)
+        lengths[rng.integers(0, count, 5)] = rng.integers(20_000, 150_000, 5)
+        offsets, end = _packed(rng, lengths, gap=int(rng.integers(0, 5)), start=int(rng.integers(0, 128)))
+        buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                              oracle.batch(buf, offsets, lengths)), k
