@@ -135,14 +135,13 @@ struct SortedWorkspace
     uint32_t* wr;        // item_cap words: a whole record's fold value, by descriptor slot
     uint32_t plog;       // log2 of the piece records longer than it are cut into (9..16)
     int ring;            // rows per ring of the hash loop: 2, 4 or 8
-    uint32_t fpw;        // full-piece slots per workgroup (sorted_full_per_wg)
     uint32_t* acc;       // fused launch (sorted_fused): 2 words per record, zero at rest; else null
 };
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);
 constexpr uint32_t kSortPieceLog2 = 16;  // 64 KiB pieces (the default)
 uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid);
-uint32_t sorted_full_per_wg(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid);
+uint64_t sorted_full_per_wg(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid);
 // batches of at most 64 cost blocks (64K records) run the hash kernel alone
 bool sorted_fused(uint64_t count);
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,

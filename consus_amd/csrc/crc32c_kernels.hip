@@ -1994,6 +1994,19 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
 // out[] word the cost kernel set to ~0.
 constexpr uint32_t kSortFuseBlocks = 64;
 
+// Full pieces one workgroup's share can hold: its items are those whose cost
+// starts in [T_b, T_b+1), at most C (1000 + w) / (1000 G) + 2 wide (the
+// XCD-weighted share, rounding included), and full pieces cost c_f = P/128 +
+// kSortFold or more each.  The host sizes the workspace with an upper bound
+// of C (total/128 + 4 items); the kernel places workgroup b's full pieces at
+// b x sorted_fpw(C, ...) from the exact C.
+__host__ __device__ inline uint64_t sorted_fpw(uint64_t C, uint32_t plog, uint64_t grid)
+{
+    const uint64_t share = C / (1000 * grid) * (1000 + kSortXcdw) +
+                           (C % (1000 * grid)) * (1000 + kSortXcdw) / (1000 * grid) + 2;
+    return share / ((uint64_t(1) << plog) / kRowBytes + kSortFold) + 3;
+}
+
 // LDS of the sorted kernel beyond the table image.
 struct SortShared
 {
@@ -2007,6 +2020,7 @@ struct SortShared
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
     uint64_t pre[2];           // cost before those blocks
     uint64_t target[2];
+    uint64_t total;            // the batch's total cost C
     uint64_t wsum[kBlock / 64];
     uint64_t fcost[kSortFuseBlocks];  // fused launches: the cost blocks, summed here
     uint32_t zinv[1024];       // Z_{-128} (the finish pass)
@@ -2084,6 +2098,7 @@ __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ bl
         T[0] = at(b);
         T[1] = at(b + 1);
     }
+    if (lane == 0) S.total = tot;
     if (lane == 0)
         for (int h = 0; h < 2; ++h)
         {
@@ -2269,9 +2284,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
-    uint32_t fpw, uint32_t* __restrict__ acc)
+    uint32_t* __restrict__ acc)
 {
-    // fpw: slots for full pieces per workgroup (items[count + b fpw ...]);
     // acc: non-null = fused launch (no sorted_cost_kernel before it), two
     // words per record, zero at rest
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
@@ -2450,14 +2464,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = e;
         if (threadIdx.x == 0)
         {
-            // full pieces go to this workgroup's own region of fpw slots (the
-            // host sizes it from a bound on any share's full pieces; round 3
-            // took them from a global cursor: a round trip in the prologue)
+            // full pieces go to this workgroup's own region of fpw slots
+            // (sorted_fpw; round 3 took them from a global cursor: a round
+            // trip in the prologue).  Every workgroup computes the same fpw
+            // from the same C, so an understated total_bytes (workspace too
+            // small) stops all of them alike: no accumulator is touched.
             const uint32_t nf = S.fbins[0] + S.fbins[1];
-            const uint32_t fb = blockIdx.x * fpw;
+            const uint64_t fpw = sorted_fpw(S.total, plog, gridDim.x);
+            const uint32_t fb = uint32_t(blockIdx.x * fpw);
             S.n_full = nf;
             S.n_items = nf + uint32_t(total);
-            if (nf > fpw || count + uint64_t(fb) + nf > item_cap)
+            if (nf > fpw || count + uint64_t(gridDim.x) * fpw > item_cap)
             {
                 ctrl[1] = 1;  // workspace too small (understated total_bytes): out[] left alone
                 S.n_items = 0;
@@ -2819,13 +2836,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 // c_f = P/128 + kSortFold apart when they are full pieces, so a share holds
 // at most share / c_f + 1 of them; C <= total/128 + 4 items bounds the total
 // cost (rows <= len/128 + 2 per item, + kSortFold).
-uint32_t sorted_full_per_wg(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid)
+uint64_t sorted_full_per_wg(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid)
 {
     const uint64_t items = count + (total_bytes >> plog) + 1;
-    const uint64_t cmax = total_bytes / kRowBytes + 4 * items;
-    const uint64_t share = cmax * (1000 + kSortXcdw) / (1000 * uint64_t(grid)) + 2;
-    const uint64_t cf = (uint64_t(1) << plog) / kRowBytes + kSortFold;
-    return uint32_t(std::min<uint64_t>(share / cf + 3, (total_bytes >> plog) + 1));
+    return sorted_fpw(total_bytes / kRowBytes + 4 * items, plog, uint64_t(grid));
 }
 
 bool sorted_fused(uint64_t count) { return sorted_blocks(count) <= kSortFuseBlocks; }
@@ -2846,7 +2860,7 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
                             : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog, ws.fpw, ws.acc);
+                       pow2, ws.plog, ws.acc);
     return hipGetLastError();
 }
 

@@ -631,7 +631,6 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
                        reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
-                       sorted_full_per_wg(count, total_bytes, plog, grid),
                        fused ? c->srt_acc.as<uint32_t>() : nullptr};
     HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
                           c->stream));
