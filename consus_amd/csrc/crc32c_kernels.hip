@@ -269,17 +269,18 @@ __device__ __forceinline__ uint4 load16(const uint8_t* p)
 }
 
 // A record's first and last rows share their 128-B lines with the
-// neighbouring records (packed back to back), which another team reads later;
-// read with the default policy those lines may stay in the MALL for it.
+// neighbouring records (packed back to back), which another team reads later.
+// The sorted kernel reads a group's edge rows (its first rows, up to the last
+// row in which an item starts, and its last row) with the default policy
+// instead of nt.  Round 4 A/B on configs[2], 3 interleaved rounds on one box:
+// 0.786-0.806 ms against 0.827-0.828 with every row nt; PMC FETCH_SIZE is
+// unchanged (2.475e6 against 2.478e6 KB x 2 per step), so the gain is in the
+// latency of those rows, not in HBM bytes (profiles/r04_sorted_edge_loads_ab.txt).
 __device__ __forceinline__ uint4 load16_edge(const uint8_t* p)
 {
-#if defined(MI_EDGE_DEFAULT)
     typedef const __attribute__((address_space(1))) u32x4_t* gptr;
     const u32x4_t v = *((gptr)(uintptr_t)p);
     return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return load16(p);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2551,13 +2552,20 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             else
             {
                 // the last of the record's pieces to arrive writes its CRC and
-                // leaves the accumulator zero for the next batch
+                // leaves the accumulator zero for the next batch.  Relaxed
+                // device-scope atomics are performed where every XCD sees
+                // them; the counter's add is issued only once this XOR has
+                // returned (the empty asm consumes its result), so the piece
+                // that counts last exchanges the complete sum.  (Acquire /
+                // release atomics here write back and invalidate the XCD's L2
+                // on every piece: 64 MiB batches took 0.117 ms instead of 0.037.)
                 uint32_t* ar = acc + 2 * uint64_t(rec);
-                __hip_atomic_fetch_xor(ar, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t was = __hip_atomic_fetch_xor(ar, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("" ::"v"(was));
                 const uint32_t n_rec = sort_cost(a_rec, L_rec, plog).n;
-                if (__hip_atomic_fetch_add(ar + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == n_rec)
+                if (__hip_atomic_fetch_add(ar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == n_rec)
                 {
-                    const uint32_t x = __hip_atomic_exchange(ar, 0u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t x = __hip_atomic_exchange(ar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(ar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     out[rec] = ~x;
                 }

@@ -84,6 +84,7 @@ while [ $# -gt 0 ]; do
                (cd /tmp && ZIPF_WARM=2 ZIPF_ROUNDS=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$v" -o k -- python3 "$ROOT/tools/zipf_probe.py" "$ROOT/tools/ab/libconsus_crc32c_$v.so" > "$OUT/fetch_$v.log" 2>&1) || { tail -5 "$OUT/fetch_$v.log"; exit 1; }
                echo "== $v (FETCH_SIZE KB x2 per dispatch, median)"; python3 tools/pmc_summary.py "$OUT/fetch_$v" crc32c_sorted_kernel sorted_cost_kernel; rm -rf "$OUT/fetch_$v"
              done | tee "$OUT/fetchab.out" ;;
+    fusedab) for fz in 1 0; do MI_CRC32C_SORT_FUSED=$fz run mid_fused$fz 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,4,16,64,256} --reps 100 || exit 1; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
