@@ -134,16 +134,13 @@ struct SortedWorkspace
     uint64_t item_cap;   // sorted_item_cap(count, total_bytes)
     uint32_t* wr;        // item_cap words: a whole record's fold value, by descriptor slot
     uint32_t plog;       // log2 of the piece records longer than it are cut into (9..16)
-    int ring;            // rows per ring of the hash loop: 2, 4 or 8
-    uint32_t* acc;       // fused launch (sorted_fused): 2 words per record, zero at rest; else null
+    int ring;            // rows per ring of the hash loop: 2 or 4
 };
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);
 constexpr uint32_t kSortPieceLog2 = 16;  // 64 KiB pieces (the default)
 uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid);
 uint64_t sorted_full_per_wg(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid);
-// batches of at most 64 cost blocks (64K records) run the hash kernel alone
-bool sorted_fused(uint64_t count);
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, const SortedWorkspace& ws,
                          uint32_t* out, const uint32_t* tables, const uint32_t* pow2, int grid,

@@ -1987,13 +1987,6 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
     }
 }
 
-// Small batches (at most kSortFuseBlocks cost blocks) skip sorted_cost_kernel:
-// every workgroup sums the block costs itself (each reads the <= 768 KB of
-// offsets and lengths from L2), finishes its own records shorter than 4 B,
-// and a split record's pieces combine through a self-cleaning accumulator
-// (the last piece to arrive writes the CRC and zeroes it) instead of an
-// out[] word the cost kernel set to ~0.
-constexpr uint32_t kSortFuseBlocks = 64;
 
 // Full pieces one workgroup's share can hold: its items are those whose cost
 // starts in [T_b, T_b+1), at most C (1000 + w) / (1000 G) + 2 wide (the
@@ -2023,7 +2016,6 @@ struct SortShared
     uint64_t target[2];
     uint64_t total;            // the batch's total cost C
     uint64_t wsum[kBlock / 64];
-    uint64_t fcost[kSortFuseBlocks];  // fused launches: the cost blocks, summed here
     uint32_t zinv[1024];       // Z_{-128} (the finish pass)
 };
 constexpr uint32_t kLdsSorted = kLdsBytes + uint32_t((sizeof(SortShared) + 255) & ~size_t(255));
@@ -2284,13 +2276,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     const uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
-    uint32_t* __restrict__ acc)
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog)
 {
-    // acc: non-null = fused launch (no sorted_cost_kernel before it), two
-    // words per record, zero at rest
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
-    const bool fused = acc != nullptr;
     const uint64_t piece = uint64_t(1) << plog;
     const uint32_t rows_max = uint32_t(piece / kRowBytes) + 1;  // rows of a full piece, unaligned
     const uint32_t lane = threadIdx.x & 63u;
@@ -2303,36 +2291,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     stage_tables(tables);  // ends with a barrier
     constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
 
-    // (0) Fused launches: the block costs (sorted_cost_kernel's sums).
-    if (fused)
-    {
-        if (threadIdx.x < kSortFuseBlocks) S.fcost[threadIdx.x] = 0;
-        __syncthreads();
-        constexpr uint32_t FB = 4;  // blocks per round, every load issued first
-        for (uint32_t j0 = 0; j0 < nb; j0 += FB)
-        {
-            uint64_t av[FB];
-            uint32_t Lv[FB];
-#pragma unroll
-            for (uint32_t q = 0; q < FB; ++q)
-            {
-                const uint64_t r = uint64_t(j0 + q) * kSortRecs + threadIdx.x;
-                av[q] = r < count ? off[r] : 0;
-                Lv[q] = r < count ? len[r] : 0;
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < FB; ++q)
-            {
-                uint64_t c = j0 + q < nb ? sort_cost(uint64_t(base) + av[q], Lv[q], plog).cost : 0;
-                for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
-                if (lane == 0 && c) atomicAdd(reinterpret_cast<unsigned long long*>(&S.fcost[j0 + q]),
-                                              (unsigned long long)c);
-            }
-        }
-        __syncthreads();
-    }
     // (1) Wave 0: the two targets and the cost blocks holding them.
-    if (threadIdx.x < 64) sort_find_blocks(fused ? S.fcost : blk_cost, nb, count, S);
+    if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S, plog);
@@ -2346,11 +2306,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // count of a wave (match_key10).  Up to 8 records per thread the ranks
     // stay in registers and the descriptors are written after the bin scan;
     // larger ranges take a second pass over the records.
-    // (a fused launch's workgroup 0 also takes the zero-cost records before the
-    // first item: records shorter than 4 B, which it finishes in the pass)
-    const bool lead0 = fused && blockIdx.x == 0;
-    const uint32_t rlo = lead0 ? 0u : S.bound[0], klo0 = lead0 ? 0u : S.bound[1];
-    const uint32_t rhi = S.bound[2], khi0 = S.bound[3];
+    const uint32_t rlo = S.bound[0], klo0 = S.bound[1], rhi = S.bound[2], khi0 = S.bound[3];
     const uint64_t rend = min(uint64_t(rhi) + (khi0 ? 1u : 0u), count);
     constexpr uint32_t U = 4, CH = 2;  // records per thread per chunk, chunks held
     const bool held = rend <= uint64_t(rlo) + U * CH * kBlock;
@@ -2430,14 +2386,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             for (uint32_t u = 0; u < U; ++u)
             {
                 const uint64_t r = c0 + u * kBlock;
-                if (fused && !second && r < rend && Lv[u] < 4)
-                {
-                    // sorted_cost_kernel's byte-serial finish of a short record
-                    const uint8_t* p = reinterpret_cast<const uint8_t*>(av[u]);
-                    uint32_t h = ~(inits ? inits[r] : 0u);
-                    for (uint32_t i = 0; i < Lv[u]; ++i) h = lds32(kLdsT + ((h ^ p[i]) & 0xFFu) * 4u) ^ (h >> 8);
-                    out[r] = ~h;
-                }
                 const RecInfo f = info(r, av[u], Lv[u]);
                 uint32_t rf, rl;
                 take(f, rf, rl);
@@ -2469,7 +2417,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             // (sorted_fpw; round 3 took them from a global cursor: a round
             // trip in the prologue).  Every workgroup computes the same fpw
             // from the same C, so an understated total_bytes (workspace too
-            // small) stops all of them alike: no accumulator is touched.
+            // small) stops all of them alike.
             const uint32_t nf = S.fbins[0] + S.fbins[1];
             const uint64_t fpw = sorted_fpw(S.total, plog, gridDim.x);
             const uint32_t fb = uint32_t(blockIdx.x * fpw);
@@ -2547,29 +2495,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             const uint64_t a_rec = uint64_t(base) + off[rec];
             const uint32_t L_rec = len[rec];
             v = zshift48(pow2, v, a_rec + L_rec - p_pe);
-            if (!fused)
-                __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-            {
-                // the last of the record's pieces to arrive writes its CRC and
-                // leaves the accumulator zero for the next batch.  Relaxed
-                // device-scope atomics are performed where every XCD sees
-                // them; the counter's add is issued only once this XOR has
-                // returned (the empty asm consumes its result), so the piece
-                // that counts last exchanges the complete sum.  (Acquire /
-                // release atomics here write back and invalidate the XCD's L2
-                // on every piece: 64 MiB batches took 0.117 ms instead of 0.037.)
-                uint32_t* ar = acc + 2 * uint64_t(rec);
-                const uint32_t was = __hip_atomic_fetch_xor(ar, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("" ::"v"(was));
-                const uint32_t n_rec = sort_cost(a_rec, L_rec, plog).n;
-                if (__hip_atomic_fetch_add(ar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == n_rec)
-                {
-                    const uint32_t x = __hip_atomic_exchange(ar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(ar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    out[rec] = ~x;
-                }
-            }
+            __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
     auto grab = [&]() {
@@ -2639,12 +2565,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
     // flight per wave while another folds (measured on the headline batch:
     // one row ahead costs < 1 % against three; here it keeps the padding to
-    // half a row per group).  RB = 4 and 8 are instantiated for small
-    // batches (pieces below 64 KiB), where a wave has only a group or two of
-    // up to 33 rows, so the rows in flight per wave, not the HBM, bound it
-    // (round 4, profiles/r04_sorted_ring_sweep.txt).  They finish whole
-    // records in the loop (no finish pass), which frees the registers RB = 8
-    // needs (128 VGPRs, no scratch).
+    // half a row per group).  RB = 4 serves small batches (pieces below
+    // 64 KiB), where a wave has only a group or two of up to 33 rows, so the
+    // rows in flight per wave, not the HBM, bound it; it finishes whole
+    // records in the loop (no finish pass).  RB = 8 (128 VGPRs once the
+    // finish pass is gone) measured no faster than 4 at 1 MiB - 2 GiB
+    // (round 4, profiles/r04_sorted_ring_sweep.txt).
     uint4 b[RB];
 #pragma unroll
     for (int j = 0; j < RB - 1; ++j) b[j] = load16_edge(row_ptr(cur0, j, false));
@@ -2850,8 +2776,6 @@ uint64_t sorted_full_per_wg(uint64_t count, uint64_t total_bytes, uint32_t plog,
     return sorted_fpw(total_bytes / kRowBytes + 4 * items, plog, uint64_t(grid));
 }
 
-bool sorted_fused(uint64_t count) { return sorted_blocks(count) <= kSortFuseBlocks; }
-
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, const SortedWorkspace& ws,
                          uint32_t* out, const uint32_t* tables, const uint32_t* pow2, int grid,
@@ -2860,15 +2784,12 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     if (count == 0) return hipSuccess;
     const uint32_t nb = sorted_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
-    if (!ws.acc)
-        hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
-                           lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
-    auto k = ws.ring == 8   ? crc32c_sorted_kernel<8>
-             : ws.ring == 4 ? crc32c_sorted_kernel<4>
-                            : crc32c_sorted_kernel<2>;
+    hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
+                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
+    auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog, ws.acc);
+                       pow2, ws.plog);
     return hipGetLastError();
 }
 
@@ -2903,8 +2824,7 @@ hipError_t configure_kernels()
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);
     const void* ks[] = {reinterpret_cast<const void*>(&crc32c_sorted_kernel<2>),
-                        reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>),
-                        reinterpret_cast<const void*>(&crc32c_sorted_kernel<8>)};
+                        reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>)};
     for (const void* f : ks)
         if (e == hipSuccess)
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSorted);

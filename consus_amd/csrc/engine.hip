@@ -327,7 +327,7 @@ struct Ctx
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
-    DevBuf srt_cost, srt_ctrl, srt_items, srt_acc;  // sorted path (launch_sorted)
+    DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
     DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
     uint32_t done_seq = 0;
     PinBuf pin_small;                   // plan-size read-back; word kDoneWord: completion word
@@ -408,7 +408,7 @@ struct Ctx
         if (stream) (void)hipStreamSynchronize(stream);
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs, &srt_cost,
-                          &srt_ctrl, &srt_items, &srt_acc, &done_ctr})
+                          &srt_ctrl, &srt_items, &done_ctr})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -591,13 +591,13 @@ uint32_t sorted_piece_log2(uint64_t total_bytes)
 // Rows in flight per wave in the sorted kernel's hash loop: 64 KiB pieces
 // (the full configs[2] batch, HBM-bound) take the 2-row ring, smaller pieces
 // (batches below 3 GiB, where a wave has a group or two) a deeper one.
-// MI_CRC32C_SORT_RING=2|4|8 overrides (A/B, tests).
+// MI_CRC32C_SORT_RING=2|4 overrides (A/B, tests).
 int sorted_ring(uint32_t plog)
 {
     if (const char* e = std::getenv("MI_CRC32C_SORT_RING"))
     {
         const int r = std::atoi(e);
-        if (r == 2 || r == 4 || r == 8) return r;
+        if (r == 2 || r == 4) return r;
     }
     return plog < kSortPieceLog2 ? kSortRingSmall : 2;
 }
@@ -615,23 +615,16 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     if (const char* e = std::getenv("MI_CRC32C_SORTED_GRID"))
         grid = std::max(1, std::min(8 * grid, std::atoi(e)));
     const uint64_t cap = sorted_item_cap(count, total_bytes, plog, grid);
-    // MI_CRC32C_SORT_FUSED=0: small batches launch sorted_cost_kernel too (A/B, tests)
-    const char* fe = std::getenv("MI_CRC32C_SORT_FUSED");
-    const bool fused = sorted_fused(count) && !(fe && !std::strcmp(fe, "0"));
     int st;
-    // ctrl[1] (overflow flag) and the fused accumulators start zero; the
-    // kernels leave the accumulators zero, the host clears a raised flag
     if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
         (st = reserve_zeroed(c->srt_ctrl, 64 * 4, c->stream)) ||
-        (st = c->srt_items.reserve(cap * 20)) ||
-        (fused && (st = reserve_zeroed(c->srt_acc, uint64_t(count) * 8, c->stream))))
+        (st = c->srt_items.reserve(cap * 20)))
         return st;
     // descriptors, then the fold values by slot
     uint8_t* const ib = c->srt_items.as<uint8_t>();
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
-                       reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
-                       fused ? c->srt_acc.as<uint32_t>() : nullptr};
+                       reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog)};
     HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
                           c->stream));
     c->sorted_ctrl = ws.ctrl;
@@ -859,8 +852,6 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         HIP_TRY(hipStreamSynchronize(c->stream));
         const bool overflow = c->sorted_ctrl ? *flag != 0 : *flag > c->plan_cap;
         if (!overflow) return MI_CRC32C_OK;
-        // a fused sorted launch runs no cost kernel to clear the flag
-        if (c->sorted_ctrl) HIP_TRY(hipMemsetAsync(c->sorted_ctrl + 1, 0, 4, c->stream));
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, 0, out))) return st;
         return finish(c, flags);
     }

@@ -3,8 +3,9 @@ one team per whole record, records binned by row count inside each
 workgroup's cost-balanced share, split records XORed together from their
 pieces.  The piece is sized by the batch (4 KiB below 192 MiB ... 64 KiB from
 3 GiB, engine.hip sorted_piece_log2); every test runs with the size's own
-piece ("auto", 4-row ring), with the 8-row ring, and with 64 KiB pieces
-forced (MI_CRC32C_SORT_PIECE_LOG2=16, the configs[2] piece, 2-row ring).  MI_CRC32C_VARPATH=sorted makes the default explicit;
+piece ("auto", 4-row ring, whole records finished in the loop), with the
+2-row ring (the finish pass), and with 64 KiB pieces forced
+(MI_CRC32C_SORT_PIECE_LOG2=16, the configs[2] piece, 2-row ring).  MI_CRC32C_VARPATH=sorted makes the default explicit;
 every result is compared with the CPU oracle, bit-exact, and the path is
 checked to have run (mi_crc32c_stats().sorted_batches).
 """
@@ -16,12 +17,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["auto", "auto-ring8", "16"], ids=["piece_auto", "piece_auto_ring8", "piece_64k"])
+@pytest.fixture(params=["auto", "auto-ring2", "16"], ids=["piece_auto", "piece_auto_ring2", "piece_64k"])
 def sorted_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
-    if request.param == "auto-ring8":
-        os.environ["MI_CRC32C_SORT_RING"] = "8"
+    if request.param == "auto-ring2":
+        os.environ["MI_CRC32C_SORT_RING"] = "2"
     elif request.param != "auto":
         os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = request.param
     before = engine.stats()["sorted_batches"]
@@ -333,14 +334,10 @@ def test_sorted_fuzz_large(engine, oracle, sorted_path, seed):
     assert sorted_path() == 1
 
 
-@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused", "cost_kernel"])
-def test_sorted_leading_and_trailing_tiny_records(engine, oracle, sorted_path, fused, monkeypatch):
+def test_sorted_leading_and_trailing_tiny_records(engine, oracle, sorted_path):
     """Records shorter than 4 B at the very start and end of the batch (zero
-    cost: no workgroup's share starts on them), split records between them.
-    A fused launch (no sorted_cost_kernel) finishes them in workgroup 0's and
-    the last workgroup's binning pass; MI_CRC32C_SORT_FUSED=0 launches the
-    cost kernel, which finishes them."""
-    monkeypatch.setenv("MI_CRC32C_SORT_FUSED", fused)
+    cost: no workgroup's share starts on them; the cost kernel finishes
+    them), split records between them."""
     rng = np.random.default_rng(61)
     lengths = np.concatenate([rng.integers(0, 4, 300), rng.integers(4, 20_000, 3000),
                               [70_000, 9000, 200_000], rng.integers(0, 4, 300)]).astype(np.uint32)
@@ -353,10 +350,9 @@ def test_sorted_leading_and_trailing_tiny_records(engine, oracle, sorted_path, f
                           oracle.batch(buf, offsets, lengths))
 
 
-def test_sorted_fused_accumulators_clean_across_batches(engine, oracle, sorted_path):
-    """The fused launch combines a split record's pieces through accumulators
-    that the last piece leaves zero: many batches in a row on one stream,
-    split records at varying positions, every result exact."""
+def test_sorted_many_batches_split_records(engine, oracle, sorted_path):
+    """Many batches in a row on one stream, split records at varying
+    positions (their pieces XOR into out[]), every result exact."""
     rng = np.random.default_rng(62)
     for k in range(12):
         count = int(rng.integers(50, 3000))
