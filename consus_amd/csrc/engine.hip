@@ -565,16 +565,20 @@ int reserve_zeroed(DevBuf& b, size_t bytes, hipStream_t stream)
 }
 
 // Piece size of the sorted path by batch size.  A team hashes one item (a
-// whole record, or a piece of a longer one) serially, one row in flight, so
-// the largest item bounds a small batch: 64 KiB pieces made every batch of
-// 1-512 MiB take 0.13-0.19 ms.  Smaller pieces cost a fold and a combine
-// each, which the full configs[2] batch pays for.  Measured (tools/mid_probe.py,
-// configs[2] records cut to size, ms per device batch; profiles/r04_sorted_piece_sweep.txt):
-//   batch     1 MiB  4 MiB  16 MiB  64 MiB  256 MiB  512 MiB  1 GiB  2 GiB  4.9 GB
-//   4 KiB     .029   .033   .034    .038    .077     .131     .237   .449   .990
-//   8 KiB     .037   .042   .042    .046    .074     .122     .213   .402   .898
-//   16 KiB    .054   .056   .062    .062    .077     .119     .209   .378   .853
-//   64 KiB    .135   .158   .155    .166    .171     .187     .250   .392   .813
+// whole record, or a piece of a longer one) serially, a few rows in flight,
+// so the largest item bounds a small batch: 64 KiB pieces made every batch
+// of 1-512 MiB take 0.13-0.19 ms.  Smaller pieces cost a fold and a combine
+// each, which the full configs[2] batch pays for.  Measured on the final
+// round-4 kernel (tools/mid_probe.py, configs[2] records cut to size, ms per
+// device batch; profiles/r04_sorted_piece_sweep.txt, last session):
+//   batch     1 MiB  16 MiB  64 MiB  256 MiB  512 MiB
+//   2 KiB     .020   .024    .034    .071     .126
+//   4 KiB     .023   .026    .031    .067     .111
+//   8 KiB     .029   .030    .034    .065     .110
+//   16 KiB    .041   .043    .045    .064     .107
+// and earlier (64 KiB pieces, round-3 kernel): 1 GiB .250, 2 GiB .392
+// against .209/.378 at 16 KiB; the full configs[2] 4.9 GB is fastest with
+// 64 KiB pieces (.813 against .853 at 16 KiB).
 // (4 against 2, ms per device batch: 1 MiB .027/.029, 16 MiB .031/.034,
 // 256 MiB .072/.074, 1 GiB .207/.218, 2 GiB .391/.395;
 // profiles/r04_sorted_ring_sweep.txt)
@@ -582,8 +586,8 @@ constexpr int kSortRingSmall = 4;
 
 uint32_t sorted_piece_log2(uint64_t total_bytes)
 {
-    if (total_bytes < (uint64_t(192) << 20)) return 12;
-    if (total_bytes < (uint64_t(384) << 20)) return 13;
+    if (total_bytes < (uint64_t(32) << 20)) return 11;
+    if (total_bytes < (uint64_t(160) << 20)) return 12;
     if (total_bytes < (uint64_t(3) << 30)) return 14;
     return kSortPieceLog2;
 }
