@@ -1873,6 +1873,8 @@ constexpr uint32_t kSortBins = kSortRows;                         // bin = kSort
 // shares.  Even workgroups take kSortXcdw/1000 more cost, odd ones as much
 // less (A/B against equal shares: 0.878-0.905 ms vs 0.885-0.916 at 20;
 // 15 is the default, 0 turns it off).
+// (round 4, with the edge-row policy: 0 / 30 measured 0.796-0.797 /
+// 0.792-0.793 ms against 0.788-0.791 at 15, profiles/r04_configs2_variants_ab.txt)
 constexpr uint32_t kSortXcdw = 15;
 constexpr uint32_t kSortFold = 2;            // cost allowance per item, in rows (fold, masks)
 constexpr uint32_t kSortPer = 1;             // records per thread of a cost block
@@ -2287,7 +2289,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x == 0) S.next_group = 0;
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
-    if (RB >= 4) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
+    // whole records finished in the loop (RB = 4, small batches) or by the
+    // finish pass (RB = 2, configs[2]: in the loop it measured 0.829-0.831
+    // ms against 0.788-0.791, profiles/r04_configs2_variants_ab.txt)
+    constexpr bool INLOOP = RB >= 4;
+    if (INLOOP) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     stage_tables(tables);  // ends with a barrier
     constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
 
@@ -2364,7 +2370,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         // a whole record's out[] holds its slot until the finish pass (whose
         // record-order reads and stores are coalesced; the loop's fold value
         // goes to wr[slot], contiguous in list order)
-        if (RB == 2 && f.last && f.s.n == 1) out[r] = lpos;
+        if (!INLOOP && f.last && f.s.n == 1) out[r] = lpos;
     };
     uint64_t ha[CH][U];
     uint32_t hL[CH][U], hf[CH][U], hl[CH][U];
@@ -2670,7 +2676,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             // whole records: the fold value by slot, eight consecutive words per
             // group (stores to out[rec] here hit a line per record, scattered:
             // 8-11 us of the configs[2] step, profiles/r03_sorted_late_finish_ab.txt)
-            if (RB == 2)
+            if (!INLOOP)
             {
                 if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
             }
@@ -2714,7 +2720,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
-    if (RB >= 4) return;  // whole records were finished in the loop
+    if (INLOOP) return;  // whole records were finished in the loop
     // Finish pass, in record order: a whole record's fold value (wr at its
     // slot) is Z_m(raw) of its bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).
     // (Split records were finished by their pieces' XORs.)

@@ -85,6 +85,7 @@ while [ $# -gt 0 ]; do
                echo "== $v (FETCH_SIZE KB x2 per dispatch, median)"; python3 tools/pmc_summary.py "$OUT/fetch_$v" crc32c_sorted_kernel sorted_cost_kernel; rm -rf "$OUT/fetch_$v"
              done | tee "$OUT/fetchab.out" ;;
     fusedab) for fz in 1 0; do MI_CRC32C_SORT_FUSED=$fz run mid_fused$fz 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,4,16,64,256} --reps 100 || exit 1; done ;;
+    zipfring) for rnd in 1 2 3; do for rg in 2 4; do echo -n "round $rnd ring $rg "; MI_CRC32C_SORT_RING=$rg timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"; done; done | tee "$OUT/zipfring.out" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
