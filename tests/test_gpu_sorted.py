@@ -362,3 +362,26 @@ def test_sorted_many_batches_split_records(engine, oracle, sorted_path):
         buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
         assert np.array_equal(_device_run(engine, buf, offsets, lengths),
                               oracle.batch(buf, offsets, lengths)), k
+
+
+@pytest.mark.parametrize("plog", [9, 11, 12, 16])
+def test_sorted_end_cut_head_keeps_init_word(engine, oracle, monkeypatch, plog):
+    """Pieces are cut from the record's end; the head (the remainder at the
+    start) keeps at least 4 bytes so the ~init word stays inside it, and a
+    shorter remainder joins the next piece.  Lengths k*P + d for d in -1..5
+    around every multiple of the piece P, at every start alignment class,
+    with inits."""
+    monkeypatch.setenv("MI_CRC32C_VARPATH", "sorted")
+    monkeypatch.setenv("MI_CRC32C_SORT_PIECE_LOG2", str(plog))
+    P = 1 << plog
+    rng = np.random.default_rng(70 + plog)
+    lens = [k * P + d for k in (1, 2, 3) for d in range(-1, 6)]
+    lengths = np.array(lens * 6 + list(rng.integers(0, 3 * P, 200)), dtype=np.uint32)
+    rng.shuffle(lengths)
+    offsets, end = _packed(rng, lengths, gap=5, start=int(rng.integers(0, 128)))
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
