@@ -1,0 +1,100 @@
+"""CPU model checks of the sorted path's piece geometry and workspace bound
+(consus_amd/csrc/crc32c_kernels.hip: sort_cost, the descriptor of piece k,
+sorted_fpw).  No GPU: the kernel's integer formulas restated in Python and
+checked by brute force over random batches.
+
+* Pieces are cut from the record's end: the full pieces are exactly P bytes
+  and end a multiple of P before the record's end (so a piece's shift is
+  Z_{P j}); the head is the remainder at the start, 4 .. P + 3 bytes (the
+  ~init word stays inside it); the pieces tile the record exactly.
+* sorted_fpw(C) bounds the full pieces any workgroup's share holds: a share is
+  the items whose cost starts in [T_b, T_b+1) with the XCD-weighted targets.
+"""
+import random
+
+ROW = 128
+FOLD = 2     # kSortFold
+XCDW = 15    # kSortXcdw
+
+
+def pieces(a, L, plog):
+    """(start, end, is_head) of each piece in cost order, or [] for L < 4."""
+    if L < 4:
+        return []
+    P = 1 << plog
+    n = (L + P - 1) >> plog
+    if n > 1 and L - ((n - 1) << plog) < 4:
+        n -= 1
+    E = a + L
+    out = []
+    for k in range(n):
+        head = k + 1 == n
+        pe = E - (((n - 1) if head else (n - 2 - k)) << plog)
+        ps = a if head else pe - P
+        out.append((ps, pe, head))
+    return out
+
+
+def rows(ps, pe):
+    return ((pe + ROW - 1) >> 7) - (ps >> 7)
+
+
+def fpw(C, plog, grid):
+    share = C // (1000 * grid) * (1000 + XCDW) + (C % (1000 * grid)) * (1000 + XCDW) // (1000 * grid) + 2
+    return share // ((1 << plog) // ROW + FOLD) + 3
+
+
+def test_end_cut_pieces_tile_the_record():
+    rnd = random.Random(1)
+    for _ in range(100_000):
+        plog = rnd.choice([9, 10, 11, 12, 14, 16])
+        P = 1 << plog
+        a = rnd.randrange(0, 1 << 20)
+        L = rnd.choice([rnd.randrange(0, 4 * P), max(0, P * rnd.randrange(1, 5) + rnd.randrange(-4, 6))])
+        ps = pieces(a, L, plog)
+        if L < 4:
+            assert ps == []
+            continue
+        span = sorted((p[0], p[1]) for p in ps)
+        assert span[0][0] == a and span[-1][1] == a + L
+        assert all(x[1] == y[0] for x, y in zip(span, span[1:]))
+        head = [p for p in ps if p[2]]
+        assert len(head) == 1 and ps[-1][2] and head[0][0] == a
+        assert 4 <= head[0][1] - head[0][0] <= P + 3
+        for p in ps[:-1]:
+            assert p[1] - p[0] == P and (a + L - p[1]) % P == 0
+        assert all(rows(p[0], p[1]) <= P // ROW + 2 for p in ps)
+
+
+def test_full_piece_regions_hold_every_share():
+    rnd = random.Random(5)
+    for _ in range(300):
+        plog = rnd.choice([9, 10, 12, 13, 14, 16])
+        grid = rnd.choice([1, 2, 3, 5, 16, 64, 256])
+        P = 1 << plog
+        items, a = [], rnd.randrange(0, 1000)
+        for _ in range(rnd.randint(1, 2500)):
+            L = rnd.choice([rnd.randrange(0, 5000), rnd.randrange(0, 300_000),
+                            P * rnd.randrange(1, 6) + rnd.randrange(-5, 5)])
+            L = max(L, 0)
+            for ps, pe, head in pieces(a, L, plog):
+                items.append((not head, rows(ps, pe) + FOLD))
+            a += L + rnd.randrange(0, 9)
+        C = sum(c for _, c in items)
+        if C == 0:
+            continue
+
+        def target(x):  # sort_find_blocks' targets
+            if x >= grid:
+                return C
+            if grid % 2 == 0:
+                return int(C * (x * 1000.0 + XCDW * (x & 1)) / (grid * 1000.0))
+            return C // grid * x + (C % grid) * x // grid
+        starts, s = [], 0
+        for full, c in items:
+            starts.append((s, full))
+            s += c
+        bound = fpw(C, plog, grid)
+        for b in range(grid):
+            t0, t1 = target(b), target(b + 1)
+            assert sum(1 for st, full in starts if full and t0 <= st < t1) <= bound

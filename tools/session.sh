@@ -53,7 +53,7 @@ while [ $# -gt 0 ]; do
              done; done | tee "$OUT/shortiso.out"; set -- ;;
     zipfpmc) C="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
              for m in full keep drop; do
-               envs="ZIPF_WARM=2 ZIPF_ROUNDS=1"; [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
+               envs="ZIPF_WARM=2 ZIPF_ROUNDS=1 MI_CRC32C_SORT_PIECE_LOG2=16 MI_CRC32C_SORT_RING=2"; [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
                (cd /tmp && env $envs timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$m" -o k -- python3 "$ROOT/tools/zipf_probe.py" > "$OUT/pmc_$m.log" 2>&1) || { tail -5 "$OUT/pmc_$m.log"; exit 1; }
                echo "== $m"; python3 tools/pmc_summary.py "$OUT/pmc_$m" crc32c_sorted_kernel sorted_cost_kernel
              done | tee "$OUT/zipfpmc.out" ;;
