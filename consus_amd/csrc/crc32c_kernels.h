@@ -135,10 +135,17 @@ struct SortedWorkspace
     uint32_t* wr;        // item_cap words: a whole record's fold value, by descriptor slot
     uint32_t plog;       // log2 of the piece records longer than it are cut into (9..16)
     int ring;            // rows per ring of the hash loop: 2 or 4
+    uint32_t lane_rows;  // records spanning <= this many rows are lane items (0..kSortLaneRowsMax)
 };
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);
 constexpr uint32_t kSortPieceLog2 = 16;  // 64 KiB pieces (the default)
+// Lane items: whole records and heads spanning at most this many 128-B rows
+// are hashed one per lane (crc32c_sorted_kernel).  configs[2], 3 interleaved
+// rounds on one box: 0.783-0.786 ms at 2 rows against 0.788-0.789 at 3 and
+// 0.792-0.799 with teams only (profiles/r04_sorted_lane_items_ab.txt).
+constexpr uint32_t kSortLaneRows = 2;
+constexpr uint32_t kSortLaneRowsMax = 3;
 uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid);
 uint64_t sorted_full_per_wg(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid);
 hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32_t* lengths,

@@ -1863,7 +1863,12 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
 constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
 // rows of the largest item: a 64 KiB + 3 B head piece at an unaligned start (514)
 constexpr uint32_t kSortRows = uint32_t(kSortPiece / kRowBytes) + 2;
-constexpr uint32_t kSortBins = kSortRows;                         // bin = kSortRows - rows
+// Lane items (round 4): whole records and heads spanning at most lrows <=
+// kSortLaneRowsMax rows are hashed one per lane (slice-by-16 over the 16-B
+// blocks they touch), binned by block count K after the team items:
+// bin = kSortRows - rows for team items, kSortRows - lrows + 8 lrows - K for
+// lane items (K <= 8 lrows).
+constexpr uint32_t kSortBins = kSortRows + 7 * kSortLaneRowsMax;
 // rows per ring of the sorted kernel: a template parameter (2 for 64 KiB pieces;
 // 4 measured slower there: profiles/r03_sorted_wave_roles_ab.txt)
 // XCD-weighted shares: workgroup b runs on XCD b % 8 (round-robin dispatch),
@@ -1893,6 +1898,7 @@ struct SortCost
     uint32_t c_int;      // cost of every piece but the last (in cost order: the full pieces)
     uint32_t rows_full;  // rows of every piece but the last
     uint32_t rows_last;  // rows of the last piece in cost order: the head
+    uint32_t blk_last;   // 16-B blocks the head touches (lane items)
 };
 
 // Pieces are cut from the record's END (round 4): the full pieces are
@@ -1907,7 +1913,7 @@ struct SortCost
 // the head last, so every piece but the last in that order costs c_int.
 __device__ __forceinline__ SortCost sort_cost(uint64_t a, uint32_t L, uint32_t plog)
 {
-    SortCost s{0, 0, 0, 0, 0};
+    SortCost s{0, 0, 0, 0, 0, 0};
     if (L < 4) return s;
     const uint64_t piece = uint64_t(1) << plog;
     s.n = uint32_t((uint64_t(L) + piece - 1) >> plog);
@@ -1916,9 +1922,23 @@ __device__ __forceinline__ SortCost sort_cost(uint64_t a, uint32_t L, uint32_t p
     s.rows_full = uint32_t(piece / kRowBytes) + ((E & (kRowBytes - 1)) ? 1u : 0u);
     const uint64_t he = E - (uint64_t(s.n - 1) << plog);  // the head's end
     s.rows_last = uint32_t(((he + kRowBytes - 1) >> 7) - (a >> 7));
+    s.blk_last = uint32_t(((he + 15) >> 4) - (a >> 4));
     s.c_int = s.rows_full + kSortFold;
     s.cost = uint64_t(s.n - 1) * s.c_int + s.rows_last + kSortFold;
     return s;
+}
+
+// The record's last item (in cost order) is a lane item.
+__device__ __forceinline__ bool sort_is_lane(const SortCost& s, uint32_t lrows)
+{
+    return s.rows_last <= lrows;
+}
+
+// Bin of the last item: team items by rows (largest first), then lane items
+// by 16-B blocks (largest first).
+__device__ __forceinline__ uint32_t sort_key(const SortCost& s, uint32_t lrows)
+{
+    return sort_is_lane(s, lrows) ? kSortRows + 7 * lrows - s.blk_last : kSortRows - s.rows_last;
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
@@ -2012,6 +2032,8 @@ struct SortShared
     uint32_t n_full;           // full pieces (listed first: the largest items)
     uint32_t full_base;        // their slots: items[count + full_base ...]
     uint32_t next_group;
+    uint32_t next_lane;        // lane items taken (64 per grab)
+    uint32_t lane_base;        // the first lane item's position among the last pieces
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
     uint64_t pre[2];           // cost before those blocks
@@ -2150,7 +2172,7 @@ __device__ __forceinline__ void sort_resolve(const uint8_t* base, const uint64_t
 #pragma unroll
     for (uint32_t q = 0; q < 2; ++q)
     {
-        sc[q] = SortCost{0, 0, 0, 0, 0};
+        sc[q] = SortCost{0, 0, 0, 0, 0, 0};
         if (j < nb && r0 + q < count)
             sc[q] = sort_cost(uint64_t(base) + off[r0 + q], len[r0 + q], plog);
         mine += sc[q].cost;
@@ -2265,6 +2287,25 @@ __device__ __forceinline__ SortView sort_view(const uint4& d, int32_t n, uint32_
     return v;
 }
 
+// The raw-CRC step over one 16-B block x (the state already XORed into its
+// first word) of which only bytes 0 .. t-1 are data (bytes >= t are zero;
+// t = 1..16): byte p goes through T_{t-1-p}; for t < 4 the state bytes
+// past the data shift down.  Lookups of p >= t read some other LDS word
+// (T_{t-1-p} < T_0: the G^{128} image) and are dropped.
+__device__ __forceinline__ uint32_t lane_tail_step(const uint4& x, uint32_t t)
+{
+    uint32_t r = t < 4u ? x.x >> (8u * t) : 0u;
+    const uint32_t tb = kLdsT + (t - 1u) * 1024u;  // T_{t-1}
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+    {
+        const uint32_t wv = p < 4 ? x.x : p < 8 ? x.y : p < 12 ? x.z : x.w;
+        const uint32_t v = lds32(tb - uint32_t(p) * 1024u + ((wv >> (8 * (p & 3))) & 0xFFu) * 4u);
+        r ^= int32_t(t) - 1 - p >= 0 ? v : 0u;
+    }
+    return r;
+}
+
 __device__ __forceinline__ uint32_t zshift48(const uint32_t* __restrict__ pow2, uint32_t v, uint64_t n)
 {
     for (int k = 0; n && k < 48; ++k, n >>= 1)
@@ -2278,7 +2319,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
     const uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog)
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
+    uint32_t lrows)
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint64_t piece = uint64_t(1) << plog;
@@ -2287,6 +2329,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = 0;
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
+    if (threadIdx.x == 0) S.next_lane = 0;
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
     // whole records finished in the loop (RB = 4, small batches) or by the
@@ -2336,7 +2379,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // count; returns (full rank or cursor, last-piece rank or cursor)
     auto take = [&](const RecInfo& f, uint32_t& rf, uint32_t& rl) {
         rf = f.nf ? atomicAdd(&S.fbins[f.s.rows_full == rows_max ? 0 : 1], f.nf) : 0u;
-        const uint32_t key = kSortRows - f.s.rows_last;
+        const uint32_t key = sort_key(f.s, lrows);
         const uint64_t eq = match_key10(key, f.last);
         const uint32_t rank = uint32_t(__builtin_popcountll(eq & ((uint64_t(1) << lane) - 1)));
         uint32_t b0 = 0;
@@ -2370,7 +2413,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         // a whole record's out[] holds its slot until the finish pass (whose
         // record-order reads and stores are coalesced; the loop's fold value
         // goes to wr[slot], contiguous in list order)
-        if (!INLOOP && f.last && f.s.n == 1) out[r] = lpos;
+        if (!INLOOP && f.last && f.s.n == 1 && !sort_is_lane(f.s, lrows)) out[r] = lpos;
     };
     uint64_t ha[CH][U];
     uint32_t hL[CH][U], hf[CH][U], hl[CH][U];
@@ -2417,6 +2460,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         uint64_t total;
         const uint32_t e = uint32_t(block_excl_scan64(c, S.wsum, total));
         if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = e;
+        if (threadIdx.x == kSortRows - lrows) S.lane_base = e;  // lane items follow the team items
         if (threadIdx.x == 0)
         {
             // full pieces go to this workgroup's own region of fpw slots
@@ -2460,7 +2504,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                         const RecInfo f = info(r, ha[c][u], hL[c][u]);
                         const uint32_t fpos = (f.s.rows_full == rows_max ? 0u : f513) + hf[c][u];
                         place(r, ha[c][u], hL[c][u], f, fpos,
-                              f.last ? S.bins[kSortRows - f.s.rows_last] + hl[c][u] : 0u);
+                              f.last ? S.bins[sort_key(f.s, lrows)] + hl[c][u] : 0u);
                     }
                 }
         }
@@ -2469,9 +2513,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     __syncthreads();
     if (n_items == 0) return;
+    // team items first, lane items (positions n_long ..) after them
+    const uint32_t n_long = n_full + S.lane_base;
 
-    // (4) Groups of 8 items, largest first, one LDS grab per group.
-    const uint32_t n_groups = (n_items + 7) / 8;
+    // (4) Groups of 8 team items, largest first, one LDS grab per group.
+    const uint32_t n_groups = (n_long + 7) / 8;
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t tw = lane / kTeam;
     const uint32_t li = lane_info();
@@ -2513,7 +2559,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint4* const listL = items + rlo - n_full;          // then the rest
     auto load_desc = [&](uint32_t g) {
         const uint32_t i = g * 8 + tw;
-        const uint4* p = (g < n_groups && i < n_items) ? (i < n_full ? listF : listL) + i
+        const uint4* p = (g < n_groups && i < n_long) ? (i < n_full ? listF : listL) + i
                                                        : reinterpret_cast<const uint4*>(zero16);
         return *p;
     };
@@ -2532,7 +2578,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto shape_of = [&](const uint4& d, uint32_t g) {
         Shape s{0, 0, 0, 0};
         if (g >= n_groups) return s;
-        const uint32_t tlast = min(7u, n_items - 1 - g * 8);
+        const uint32_t tlast = min(7u, n_long - 1 - g * 8);
         const int rv = int(sort_rows(d));
         int32_t rmax = 0, rmin = int32_t(kSortRows);
 #pragma unroll
@@ -2554,6 +2600,95 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         return p;
     };
 
+    // (5) Lane items, 64 per grab, one per lane (lane
+    // items).  A lane hashes the 16-B aligned blocks its item touches with
+    // the slice-by-16 tables: bytes before the item are zeroed (leading zeros
+    // leave the zero raw state at zero), ~init is XORed over its first 4
+    // bytes, and the last block, holding t = 1..16 of the item's bytes, takes
+    // the t-byte form of the step, so the state is the item's raw CRC with no
+    // finish.  The list is ordered by block count, so the lanes of a wave run
+    // about the same number of steps.  Blocks are read with the default
+    // policy: a block's line is shared with the neighbouring records.
+    auto lane_items = [&]() {
+        const uint32_t n_lane = n_items - n_long;
+        const uint4* const listLane = listL + n_long;
+        for (;;)
+        {
+            uint32_t c0 = 0;
+            if (lane == 0) c0 = atomicAdd(&S.next_lane, 64u);
+            c0 = uint32_t(__builtin_amdgcn_readfirstlane(int(c0)));
+            if (c0 >= n_lane) break;
+            const bool act = c0 + lane < n_lane;
+            const uint4 d = act ? listLane[c0 + lane] : make_uint4(0, 0, 0, 0);
+            const uint64_t a = uint64_t(d.x) | (uint64_t(d.y) << 32);
+            const uint64_t e = a + d.z;
+            const uint32_t q = uint32_t(a) & 15u;
+            const int32_t K = act ? int32_t(((e + 15) >> 4) - (a >> 4)) : 0;  // blocks, >= 1
+            const uint32_t t = ((uint32_t(e) - 1u) & 15u) + 1u;                // item bytes' end in the last block
+            const uint32_t rec = d.w & kSortRecMask;
+            const bool with_init = !(d.w & kSortMulti) || (d.w & kSortFirst);
+            const uint32_t ninit = !with_init ? 0u : inits ? (act ? ~inits[rec] : 0u) : 0xFFFFFFFFu;
+            const uint64_t shi = uint64_t(ninit) << ((q & 3u) * 8u);
+            const uint32_t xl = uint32_t(shi), xh = uint32_t(shi >> 32);
+            const uint32_t qd = q >> 2;
+            const uint4 xf = make_uint4(qd == 0 ? xl : 0u, qd == 1 ? xl : qd == 0 ? xh : 0u,
+                                        qd == 2 ? xl : qd == 1 ? xh : 0u, qd == 3 ? xl : qd == 2 ? xh : 0u);
+            const uint32_t xs = qd == 3 ? xh : 0u;  // the init word's spill into block 1
+            const uint4 kf = make_uint4(keep_from(int32_t(q), 0), keep_from(int32_t(q), 1),
+                                        keep_from(int32_t(q), 2), keep_from(int32_t(q), 3));
+            const uint8_t* const pb = reinterpret_cast<const uint8_t*>(a & ~uint64_t(15));
+            const int32_t nb = K - 1;  // blocks before the last
+            uint32_t st = 0;
+            // four blocks per step, all loads first
+            for (int32_t j = 0; __builtin_amdgcn_ballot_w64(j < nb) != 0; j += 4)
+            {
+                uint4 w[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    w[u] = load16_edge(j + u < nb ? pb + 16 * (j + u) : zero16);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                {
+                    uint4 x = w[u];
+                    if (j + u == 0)
+                    {
+                        x.x = __builtin_amdgcn_bitop3_b32(x.x, kf.x, xf.x, 0x6A);
+                        x.y = __builtin_amdgcn_bitop3_b32(x.y, kf.y, xf.y, 0x6A);
+                        x.z = __builtin_amdgcn_bitop3_b32(x.z, kf.z, xf.z, 0x6A);
+                        x.w = __builtin_amdgcn_bitop3_b32(x.w, kf.w, xf.w, 0x6A);
+                    }
+                    if (j + u == 1) x.x ^= xs;
+                    const uint32_t sn = zT<4>(st ^ x.x) ^ zT<3>(x.y) ^ zT<2>(x.z) ^ zT<1>(x.w);
+                    st = j + u < nb ? sn : st;
+                }
+            }
+            // the last block: bytes >= t zeroed, then the t-byte step
+            {
+                uint4 x = load16_edge(act ? pb + 16 * (K - 1) : zero16);
+                const bool first = K == 1;
+                x.x = first ? __builtin_amdgcn_bitop3_b32(x.x, kf.x, xf.x, 0x6A) : x.x;
+                x.y = first ? __builtin_amdgcn_bitop3_b32(x.y, kf.y, xf.y, 0x6A) : x.y;
+                x.z = first ? __builtin_amdgcn_bitop3_b32(x.z, kf.z, xf.z, 0x6A) : x.z;
+                x.w = first ? __builtin_amdgcn_bitop3_b32(x.w, kf.w, xf.w, 0x6A) : x.w;
+                x.x ^= K == 2 ? xs : 0u;
+                x = mask_below(x, int32_t(t));
+                x.x ^= st;
+                st = lane_tail_step(x, t);
+            }
+            if (act)
+            {
+                if (!(d.w & kSortMulti))
+                    out[rec] = ~st;
+                else
+                {
+                    // the head of a split record: Z_{E - pe}(raw(head)), E the record's end
+                    const uint64_t E = uint64_t(base) + off[rec] + len[rec];
+                    __hip_atomic_fetch_xor(out + rec, zshift48(pow2, st, E - e), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    };
     uint32_t g_cur = grab();
     uint4 d_cur = load_desc(g_cur);
     uint32_t g_nxt = grab();
@@ -2720,6 +2855,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
+
+    lane_items();
     if (INLOOP) return;  // whole records were finished in the loop
     // Finish pass, in record order: a whole record's fold value (wr at its
     // slot) is Z_m(raw) of its bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).
@@ -2751,7 +2888,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             const uint64_t r = r0 + u * kBlock;
             const RecInfo f = info(r, av[u], Lv[u]);
-            own[u] = r < rend && f.s.n == 1 && f.last;
+            own[u] = r < rend && f.s.n == 1 && f.last && !sort_is_lane(f.s, lrows);
             wv[u] = own[u] ? wr[uint64_t(rlo) + sv[u]] : 0u;
         }
 #pragma unroll
@@ -2795,7 +2932,7 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog);
+                       pow2, ws.plog, ws.lane_rows);
     return hipGetLastError();
 }
 

@@ -606,6 +606,16 @@ int sorted_ring(uint32_t plog)
     return plog < kSortPieceLog2 ? kSortRingSmall : 2;
 }
 
+// Records spanning at most this many 128-B rows are hashed one per lane
+// (lane items); MI_CRC32C_SORT_LANE_ROWS=0..3
+// overrides (0: every item takes a team).
+uint32_t sorted_lane_rows()
+{
+    if (const char* e = std::getenv("MI_CRC32C_SORT_LANE_ROWS"))
+        return uint32_t(std::max(0, std::min(int(kSortLaneRowsMax), std::atoi(e))));
+    return kSortLaneRows;
+}
+
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
 int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
@@ -628,7 +638,8 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     uint8_t* const ib = c->srt_items.as<uint8_t>();
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
-                       reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog)};
+                       reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
+                       sorted_lane_rows()};
     HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
                           c->stream));
     c->sorted_ctrl = ws.ctrl;

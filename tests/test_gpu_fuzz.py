@@ -99,7 +99,10 @@ def test_fuzz_round(engine, oracle, round_):
     grid = [None, "1", "2", "5", "64"][int(rng.integers(0, 5))]
     plog = [None, "9", "10", "12", "13", "14", "16"][int(rng.integers(0, 7))]
     ring = [None, "2", "4"][int(rng.integers(0, 3))]
+    lanes = [None, "0", "1", "3"][int(rng.integers(0, 4))]  # rows of a lane item (default 2)
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
+    if lanes:
+        os.environ["MI_CRC32C_SORT_LANE_ROWS"] = lanes
     if ring:
         os.environ["MI_CRC32C_SORT_RING"] = ring
     if grid:
@@ -110,13 +113,14 @@ def test_fuzz_round(engine, oracle, round_):
         before = engine.stats()["sorted_batches"]
         engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini,
                             total_bytes=max(int(lengths.sum(dtype=np.uint64)), 1))
-        assert np.array_equal(d_out.download(np.uint32, count), want), ("sorted", grid, plog, ring)
+        assert np.array_equal(d_out.download(np.uint32, count), want), ("sorted", grid, plog, ring, lanes)
         assert engine.stats()["sorted_batches"] == before + 1
     finally:
         os.environ.pop("MI_CRC32C_VARPATH", None)
         os.environ.pop("MI_CRC32C_SORTED_GRID", None)
         os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
         os.environ.pop("MI_CRC32C_SORT_RING", None)
+        os.environ.pop("MI_CRC32C_SORT_LANE_ROWS", None)
 
     # single buffers: one record on the host and on the device
     i = int(rng.integers(0, count))

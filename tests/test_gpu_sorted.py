@@ -5,7 +5,9 @@ pieces.  The piece is sized by the batch (4 KiB below 192 MiB ... 64 KiB from
 3 GiB, engine.hip sorted_piece_log2); every test runs with the size's own
 piece ("auto", 4-row ring, whole records finished in the loop), with the
 2-row ring (the finish pass), and with 64 KiB pieces forced
-(MI_CRC32C_SORT_PIECE_LOG2=16, the configs[2] piece, 2-row ring).  MI_CRC32C_VARPATH=sorted makes the default explicit;
+(MI_CRC32C_SORT_PIECE_LOG2=16, the configs[2] piece, 2-row ring), the last
+also with lane items off (MI_CRC32C_SORT_LANE_ROWS=0: records of <= 2 rows
+take teams too).  MI_CRC32C_VARPATH=sorted makes the default explicit;
 every result is compared with the CPU oracle, bit-exact, and the path is
 checked to have run (mi_crc32c_stats().sorted_batches).
 """
@@ -17,18 +19,23 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["auto", "auto-ring2", "16"], ids=["piece_auto", "piece_auto_ring2", "piece_64k"])
+@pytest.fixture(params=["auto", "auto-ring2", "16", "16-nolane"],
+                ids=["piece_auto", "piece_auto_ring2", "piece_64k", "piece_64k_teams_only"])
 def sorted_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
     if request.param == "auto-ring2":
         os.environ["MI_CRC32C_SORT_RING"] = "2"
+    elif request.param == "16-nolane":
+        os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = "16"
+        os.environ["MI_CRC32C_SORT_LANE_ROWS"] = "0"
     elif request.param != "auto":
         os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = request.param
     before = engine.stats()["sorted_batches"]
     yield lambda: engine.stats()["sorted_batches"] - before
     os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
     os.environ.pop("MI_CRC32C_SORT_RING", None)
+    os.environ.pop("MI_CRC32C_SORT_LANE_ROWS", None)
     if old is None:
         del os.environ["MI_CRC32C_VARPATH"]
     else:
@@ -385,3 +392,27 @@ def test_sorted_end_cut_head_keeps_init_word(engine, oracle, monkeypatch, plog):
                           oracle.batch(buf, offsets, lengths, inits))
     assert np.array_equal(_device_run(engine, buf, offsets, lengths),
                           oracle.batch(buf, offsets, lengths))
+
+
+@pytest.mark.parametrize("plog", [None, "9"])
+def test_sorted_lane_items_every_shape(engine, oracle, sorted_path, plog, monkeypatch):
+    """Lane items (records spanning <= 2 rows, one per lane): every length
+    4..400 at every start offset mod 16, with and without inits, mixed with
+    team items; with 512-B pieces (plog 9) also split records whose short
+    heads are lane items (their part shifted by Z_{E - pe} and XORed in)."""
+    if plog:
+        monkeypatch.setenv("MI_CRC32C_SORT_PIECE_LOG2", plog)
+    rng = np.random.default_rng(77)
+    lens = [L for L in range(4, 401) for _ in range(2)]
+    lens += [512 * k + h for k in (1, 2, 5) for h in range(4, 140, 3)]  # short heads at plog 9
+    lens += list(rng.integers(0, 3000, 500))
+    lengths = np.array(lens, dtype=np.uint32)
+    rng.shuffle(lengths)
+    offsets, end = _packed(rng, lengths, gap=15, start=int(rng.integers(0, 16)))
+    buf = rng.integers(0, 256, end + 32, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths),
+                          oracle.batch(buf, offsets, lengths))
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+    assert sorted_path() == 2

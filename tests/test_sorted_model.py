@@ -98,3 +98,82 @@ def test_full_piece_regions_hold_every_share():
         for b in range(grid):
             t0, t1 = target(b), target(b + 1)
             assert sum(1 for st, full in starts if full and t0 <= st < t1) <= bound
+
+
+# --- lane items: one record per lane, slice-by-16 over its aligned 16-B blocks
+
+POLY = 0x82F63B78
+
+
+def _tables():
+    t0 = []
+    for b in range(256):
+        c = b
+        for _ in range(8):
+            c = (c >> 1) ^ (POLY if c & 1 else 0)
+        t0.append(c)
+    T = [t0]
+    for _ in range(15):
+        T.append([(v >> 8) ^ t0[v & 0xFF] for v in T[-1]])
+    return T
+
+
+def _bitwise_crc(init, data):
+    c = init ^ 0xFFFFFFFF
+    for byte in data:
+        c ^= byte
+        for _ in range(8):
+            c = (c >> 1) ^ (POLY if c & 1 else 0)
+    return c ^ 0xFFFFFFFF
+
+
+def lane_item(T, buf, a, L, init):
+    """The lane loop of crc32c_sorted_kernel, restated: blocks [a & ~15, ...),
+    bytes before a zeroed, ~init over bytes a..a+3, the last block's t-byte
+    step (lane_tail_step)."""
+    e = a + L
+    q = a & 15
+    K = ((e + 15) >> 4) - (a >> 4)
+    t = ((e - 1) & 15) + 1
+    c0 = a & ~15
+    ninit = init ^ 0xFFFFFFFF
+
+    def block(j):
+        x = bytearray(buf[c0 + 16 * j: c0 + 16 * j + 16])
+        x += bytes(16 - len(x))
+        for p in range(16):  # head: zero before a, ~init over the first 4 bytes
+            pos = c0 + 16 * j + p
+            if pos < a:
+                x[p] = 0
+            elif pos < a + 4:
+                x[p] ^= (ninit >> (8 * (pos - a))) & 0xFF
+        return x
+
+    st = 0
+    for j in range(K - 1):
+        x = block(j)
+        w0 = int.from_bytes(x[:4], "little") ^ st
+        x[:4] = w0.to_bytes(4, "little")
+        st = 0
+        for p in range(16):
+            st ^= T[15 - p][x[p]]
+    x = block(K - 1)
+    for p in range(t, 16):
+        x[p] = 0
+    w0 = int.from_bytes(x[:4], "little") ^ st
+    x[:4] = w0.to_bytes(4, "little")
+    r = (w0 >> (8 * t)) if t < 4 else 0
+    for p in range(t):
+        r ^= T[t - 1 - p][x[p]]
+    return r ^ 0xFFFFFFFF
+
+
+def test_lane_item_step_matches_crc32c():
+    T = _tables()
+    rnd = random.Random(11)
+    buf = bytes(rnd.randrange(256) for _ in range(2048))
+    for _ in range(3000):
+        L = rnd.choice([rnd.randrange(4, 40), rnd.randrange(4, 400)])
+        a = rnd.randrange(0, len(buf) - L)
+        init = rnd.choice([0, 0xFFFFFFFF, rnd.randrange(1 << 32)])
+        assert lane_item(T, buf, a, L, init) == _bitwise_crc(init, buf[a:a + L]), (a, L, init)

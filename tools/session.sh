@@ -50,7 +50,20 @@ while [ $# -gt 0 ]; do
                set -- $cfg; v=$1; m=$2; envs="MI_CRC32C_SORT_SHORT=$v"
                [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
                echo -n "round $rnd short=$v class=$m "; env $envs timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
-             done; done | tee "$OUT/shortiso.out"; set -- ;;
+             done; done | tee "$OUT/shortiso.out" ;;
+    laneab) for rnd in 1 2 3; do for v in 0 1 2 3; do
+               echo -n "round $rnd lane_rows=$v "; MI_CRC32C_SORT_LANE_ROWS=$v timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done; done | tee "$OUT/laneab.out" ;;
+    lanekeep) for rnd in 1 2; do for k in 257 1024; do for v in 0 2 3; do
+               echo -n "round $rnd keep<$k lane_rows=$v "; ZIPF_KEEP_BELOW=$k MI_CRC32C_SORT_LANE_ROWS=$v timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done; done; done | tee "$OUT/lanekeep.out" ;;
+    lanepmc) C="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+             for v in 0 2; do
+               envs="ZIPF_WARM=2 ZIPF_ROUNDS=1 ZIPF_KEEP_BELOW=257 MI_CRC32C_SORT_LANE_ROWS=$v"
+               (cd /tmp && env $envs timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_l$v" -o k -- python3 "$ROOT/tools/zipf_probe.py" > "$OUT/pmc_l$v.log" 2>&1) || { tail -5 "$OUT/pmc_l$v.log"; exit 1; }
+               echo "== keep<257 lane_rows=$v"; python3 tools/pmc_summary.py "$OUT/pmc_l$v" crc32c_sorted_kernel
+             done | tee "$OUT/lanepmc.out" ;;
+    lanetests) run pytest_lane 600 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread ;;
     zipfpmc) C="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
              for m in full keep drop; do
                envs="ZIPF_WARM=2 ZIPF_ROUNDS=1 MI_CRC32C_SORT_PIECE_LOG2=16 MI_CRC32C_SORT_RING=2"; [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
