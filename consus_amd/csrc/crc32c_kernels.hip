@@ -2337,12 +2337,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // ms against 0.788-0.791, profiles/r04_configs2_variants_ab.txt)
     constexpr bool INLOOP = RB >= 4;
     if (INLOOP) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
+    // (1) Wave 0: the two targets and the cost blocks holding them, while the
+    // other waves stage the tables (the staging's barrier covers both).
+    if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     stage_tables(tables);  // ends with a barrier
     constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
-
-    // (1) Wave 0: the two targets and the cost blocks holding them.
-    if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
-    __syncthreads();
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S, plog);
 
