@@ -177,3 +177,26 @@ def test_lane_item_step_matches_crc32c():
         a = rnd.randrange(0, len(buf) - L)
         init = rnd.choice([0, 0xFFFFFFFF, rnd.randrange(1 << 32)])
         assert lane_item(T, buf, a, L, init) == _bitwise_crc(init, buf[a:a + L]), (a, L, init)
+
+
+def test_lane_and_team_bins_are_disjoint_and_ordered():
+    """sort_key: team items by rows (kSortRows - rows), lane items after them
+    by 16-B blocks (kSortRows + 7 lrows - K), inside kSortBins = kSortRows +
+    7 * 3 bins; K <= 8 * rows, so a lane key never meets a team key."""
+    k_rows, lmax = 65536 // ROW + 2, 3
+    bins = k_rows + 7 * lmax
+    rnd = random.Random(3)
+    for _ in range(20_000):
+        lrows = rnd.randrange(0, lmax + 1)
+        a = rnd.randrange(0, 1 << 20)
+        L = rnd.randrange(4, 1200)
+        e = a + L
+        rows = ((e + ROW - 1) >> 7) - (a >> 7)
+        K = ((e + 15) >> 4) - (a >> 4)
+        assert K <= 8 * rows
+        if rows <= lrows:
+            key = k_rows + 7 * lrows - K
+            assert k_rows - lrows <= key < bins
+        else:
+            key = k_rows - rows
+            assert 0 <= key < k_rows - lrows
