@@ -2340,7 +2340,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // (1) Wave 0: the two targets and the cost blocks holding them, while the
     // other waves stage the tables (the staging's barrier covers both).
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
-    stage_tables(tables);  // ends with a barrier
+    __syncthreads();
+    // The tables are staged after the binning (step 3), which uses their LDS
+    // to put the descriptors in list order first.
     constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S, plog);
@@ -2406,9 +2408,24 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto put = [&](uint4* dst, const uint4& dv) {
         __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
     };
+    // Up to kLdsBytes / 16 items, the descriptors go to LDS at their list
+    // position (the table image's space: the tables are staged after), and
+    // then out in list order, whole lines: scattered 16-B stores cost the
+    // configs[2] prologue 19 us (profiles/r04_sorted_prologue_phases.txt).
+    uint4* const stage_lds = reinterpret_cast<uint4*>(smem);
+    bool staged = false;
+    uint32_t stage_nf = 0;
+    auto put_full = [&](uint32_t pos, const uint4& dv) {
+        if (staged) stage_lds[pos] = dv;
+        else put(fullv + S.full_base + pos, dv);
+    };
+    auto put_last = [&](uint32_t pos, const uint4& dv) {
+        if (staged) stage_lds[stage_nf + pos] = dv;
+        else put(lastv + pos, dv);
+    };
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
-        for (uint32_t i = 0; i < f.nf; ++i) put(fullv + S.full_base + fpos + i, desc(r, a, L, f, f.klo + i));
-        if (f.last) put(lastv + lpos, desc(r, a, L, f, f.s.n - 1));
+        for (uint32_t i = 0; i < f.nf; ++i) put_full(fpos + i, desc(r, a, L, f, f.klo + i));
+        if (f.last) put_last(lpos, desc(r, a, L, f, f.s.n - 1));
         // a whole record's out[] holds its slot until the finish pass (whose
         // record-order reads and stores are coalesced; the loop's fold value
         // goes to wr[slot], contiguous in list order)
@@ -2487,6 +2504,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     __syncthreads();
     const uint32_t n_items = S.n_items, n_full = S.n_full;
+    staged = n_items <= kLdsBytes / 16;
+    stage_nf = n_full;
     if (n_items)
     {
         if (held)
@@ -2512,6 +2531,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     __syncthreads();
     if (n_items == 0) return;
+    if (staged)
+    {
+        // list order out: full pieces to their region, the rest after rlo
+        for (uint32_t i = threadIdx.x; i < n_items; i += kBlock)
+            put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
+        __syncthreads();
+    }
+    stage_tables(tables);  // ends with a barrier
     // team items first, lane items (positions n_long ..) after them
     const uint32_t n_long = n_full + S.lane_base;
 
