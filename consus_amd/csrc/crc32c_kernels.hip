@@ -1848,16 +1848,22 @@ hipError_t launch_single(const void* data, uint64_t h, uint64_t m, uint32_t t, u
 //       4 B are finished here byte-serially; split records get out[r] = ~0.
 //   crc32c_sorted_kernel: with C the total cost and G workgroups, workgroup b
 //       takes the items whose cost starts in [C b / G, C (b + 1) / G), a
-//       contiguous run of records.  It bins them by row count in LDS (largest
-//       first), writes 16-B descriptors to the workspace, and its 16 waves
-//       take groups of 8 items (one per team) from an LDS counter, largest
-//       first (LPT).  A team hashes its item's 128-B rows right-aligned to the
-//       group's row count (padded to an even count for the two-row ring):
-//       ~init is XORed into the record's first 4 bytes
-//       (identity 3), bytes outside the item are masked, rows before it are
-//       read from a zero block, and crc = ~Z_{-m}(fold), m = ceil128(E) - E.
-//   Records longer than 64 KiB are cut into 64 KiB pieces from their start;
-//   each piece XORs Z_{E - pe}(raw(piece)) into out[r] (identity 1).
+//       contiguous run of records.  It bins them by row count (largest
+//       first; items of <= lrows rows after them, by 16-B block count),
+//       builds the 16-B descriptor list in LDS (before the tables are
+//       staged there) and writes it to the workspace in list order.  Its 16
+//       waves take groups of 8 team items (one per team) from an LDS
+//       counter, largest first (LPT).  A team hashes its item's 128-B rows
+//       right-aligned to the group's row count (padded to a multiple of the
+//       ring): ~init is XORed into the record's first 4 bytes (identity 3),
+//       bytes outside the item are masked, rows before it are read from a
+//       zero block, and crc = ~Z_{-m}(fold), m = ceil128(E) - E (in the loop
+//       for the 4-row ring, else by a finish pass in record order).  Then
+//       the lane items, 64 per grab, one per lane: slice-by-16 over the
+//       blocks, no fold, no finish.
+//   Records longer than a piece (2-64 KiB, by batch size) are cut into
+//   pieces from their end; each piece XORs Z_{E - pe}(raw(piece)) into
+//   out[r] (identity 1).
 // No plan/finalize passes over the items: one small launch, then the hash.
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSortPiece = 65536;                            // bytes per piece of a split record
@@ -2040,7 +2046,7 @@ struct SortShared
     uint64_t target[2];
     uint64_t total;            // the batch's total cost C
     uint64_t wsum[kBlock / 64];
-    uint32_t zinv[1024];       // Z_{-128} (the finish pass)
+    uint32_t zinv[1024];       // Z_{-128} (the finish, in the loop or after it)
 };
 constexpr uint32_t kLdsSorted = kLdsBytes + uint32_t((sizeof(SortShared) + 255) & ~size_t(255));
 static_assert(kLdsSorted <= 163840, "sorted kernel LDS");
