@@ -416,3 +416,21 @@ def test_sorted_lane_items_every_shape(engine, oracle, sorted_path, plog, monkey
     assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
                           oracle.batch(buf, offsets, lengths, inits))
     assert sorted_path() == 2
+
+
+@pytest.mark.parametrize("count", [8500, 9728, 9729, 9900])
+def test_sorted_descriptor_staging_limits(engine, oracle, sorted_path, count):
+    """One workgroup holding 8,500-9,900 items: the descriptor list is staged
+    in LDS up to kLdsBytes / 16 = 9,728 items (above 8,192 records through the
+    binning's second pass) and stored directly above that."""
+    rng = np.random.default_rng(count)
+    lengths = rng.integers(4, 700, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths, gap=3, start=5)
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32)
+    os.environ["MI_CRC32C_SORTED_GRID"] = "1"
+    try:
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                              oracle.batch(buf, offsets, lengths, inits))
+    finally:
+        del os.environ["MI_CRC32C_SORTED_GRID"]
