@@ -234,13 +234,16 @@ def rccl_gather(E, dist, rank: int, world: int, out, R: int, digests, rec) -> di
     it stays valid: the gather is outside the timed region)."""
     import threading
     done = threading.Event()
+    # BENCH_GATHER_TIMEOUT_S: the watchdog's limit (tests/test_bench_multirank.py
+    # drives the hung-collective exit with a short one)
+    limit = float(os.environ.get("BENCH_GATHER_TIMEOUT_S", "120"))
 
     def watchdog():
-        if not done.wait(120.0):
+        if not done.wait(limit):
             if rec is not None:
-                rec["gather"] = {"collective": "rccl all-gather", "error": "timed out after 120 s"}
+                rec["gather"] = {"collective": "rccl all-gather", "error": f"timed out after {limit:g} s"}
                 print(json.dumps(rec), flush=True)
-            print(f"rank {rank}: RCCL gather timed out after 120 s", file=sys.stderr, flush=True)
+            print(f"rank {rank}: RCCL gather timed out after {limit:g} s", file=sys.stderr, flush=True)
             os._exit(3)
     threading.Thread(target=watchdog, daemon=True).start()
     try:
@@ -1121,6 +1124,8 @@ def main():
     code = 0
     if world > 1:
         rec["roofline"]["launch_ms_rank0"] = round(ev_ms / args.steps, 4)
+        # the ranks' identities first: a hung gather's watchdog prints this line
+        multi_rank_fields(rec, ranks, None, world, args.share_device)
         gather = rccl_gather(E, dist, rank, world, out, R, digests, rec) if do_gather else None
         code = multi_rank_fields(rec, ranks, gather, world, args.share_device)
     print(json.dumps(rec), flush=True)

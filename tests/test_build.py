@@ -78,3 +78,53 @@ def test_no_scalar_cache_writes(asm):
     pat = r"^\s*(s_(?:" + "|".join(fam) + r")\w*)"
     bad = re.findall(pat, asm, re.M)
     assert not bad, sorted(set(bad))
+
+
+def test_clean_tree_build_from_source(tmp_path):
+    """build() runs `make`, which may reuse an up-to-date in-tree library.  This
+    proves the sources compile: the engine library rebuilt from scratch
+    (`make -B`) into a temporary directory, its gfx950 code object unbundled
+    from the library's fat binary and its kernel metadata checked, and every
+    symbol the headers declare exported by the fresh library."""
+    import ctypes
+
+    from test_abi import declared_functions
+
+    obj, lib = tmp_path / "obj", tmp_path / "lib" / "libconsus_crc32c.so"
+    r = subprocess.run(["make", "-s", "-B", "-j8", "-C", os.path.join(REPO, "consus_amd", "csrc"),
+                        f"BUILD={obj}", f"OUT={lib}", str(lib)],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert lib.exists() and sorted(p.name for p in obj.iterdir()) == sorted(
+        ["api.o", "crc32c_kernels.o", "durable_log.o", "engine.o", "host_crc.o", "workload.o"])
+    llvm = "/opt/rocm/lib/llvm/bin/"
+    fat, co = tmp_path / "fat.bin", tmp_path / "co.elf"
+    subprocess.run([llvm + "llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", str(lib), os.devnull],
+                   check=True, timeout=120)
+    bundles = subprocess.run([llvm + "clang-offload-bundler", "--list", "--type=o", f"--input={fat}"],
+                             capture_output=True, text=True, check=True, timeout=120).stdout.split()
+    assert "hipv4-amdgcn-amd-amdhsa--gfx950" in bundles, bundles
+    assert not [b for b in bundles if "amdgcn" in b and not b.endswith("gfx950")], bundles
+    subprocess.run([llvm + "clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"],
+                   check=True, timeout=120)
+    notes = subprocess.run([llvm + "llvm-readelf", "--notes", str(co)], capture_output=True,
+                           text=True, check=True, timeout=120).stdout
+    assert "amdgcn-amd-amdhsa--gfx950" in notes
+    # one metadata map per kernel: name, VGPRs, scratch, static LDS
+    kern = {}
+    for blk in re.split(r"\n\s+- \.", notes):
+        name = re.search(r"\.name:\s+(\S+)", blk)
+        if name and "_ZN6mi_crc" in name.group(1):
+            kern[name.group(1)] = {k: int(v) for k, v in re.findall(
+                r"\.(vgpr_count|private_segment_fixed_size|group_segment_fixed_size):\s+(\d+)", blk)}
+    for must in ("crc32c_fixed_pipe_kernel", "crc32c_sorted_kernel", "crc32c_direct_kernel",
+                 "sorted_cost_kernel", "crc32c_combine_kernel"):
+        assert any(must in k for k in kern), (must, sorted(kern))
+    for k, f in kern.items():
+        if any(n in k for n in ("crc32c_fixed_pipe_kernel", "crc32c_sorted_kernel")):
+            assert f["vgpr_count"] <= 128 and f["private_segment_fixed_size"] == 0, (k, f)
+            assert f["group_segment_fixed_size"] == 0, (k, f)  # dynamic LDS image only
+    fresh = ctypes.CDLL(str(lib))
+    missing = [n for n in declared_functions() if not hasattr(fresh, n)]
+    assert not missing, missing
