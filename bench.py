@@ -398,114 +398,164 @@ def cpu_baseline(args) -> dict:
             "first_crc": int(crc_ref[0])}
 
 
+def _interp(points, n):
+    """Linear interpolation of {bytes: us} at n bytes (clamped to the ends)."""
+    pts = sorted((int(k), float(v)) for k, v in points.items())
+    if not pts:
+        return None
+    if n <= pts[0][0]:
+        return pts[0][1] * n / pts[0][0]
+    for (n0, t0), (n1, t1) in zip(pts, pts[1:]):
+        if n <= n1:
+            return t0 + (t1 - t0) * (n - n0) / (n1 - n0)
+    (n0, t0), (n1, t1) = pts[-2], pts[-1]
+    return t1 + (t1 - t0) * (n - n1) / (n1 - n0)
+
+
 def run_dlog(args, compact: bool = False) -> dict:
     """The batching durable log driven as txman drives it (tools/dlog_bench.cc):
-    8 threads append 400K entries each (42-1024 B), the caller waits for the
-    watermark to cover them, then the log is replayed (GPU-verified scan of
-    both segment files) and every record checked byte-exact.  Segment files
-    on tmpfs (/dev/shm): fsync is free there, so this is the front-end and
-    batch-CRC rate, not a disk's.  Same run, interleaved: the same front-end
-    with the reference common/crc32c.cc (oracle/_ref) as the flush thread's
-    checksum (txman/durable_log.cc:187-242 calls it per record) -- the CPU
-    baseline of this line."""
+    8 threads append concurrently, the caller waits for the watermark to cover
+    every record, then the log is replayed (GPU-verified scan of both segment
+    files) and every record checked byte-exact.  Segment files on tmpfs
+    (/dev/shm): fsync is free there, so this is the front-end and checksum
+    rate, not a disk's.  Two entry-length workloads: uniform 42-1024 B, and
+    configs[2]'s Zipf 64 B - 64 KiB (where one core's crc32q is a real cost).
+    Four engines, runs interleaved (>= 7 each), median and IQR reported:
+      gpu               the batching front-end, one GPU batch per flushed
+                        segment (flushes below the measured GPU/CPU crossover
+                        on the flush thread's CPU path, counted);
+      reference-scheme  the reference's own placement (txman/durable_log.cc:
+                        215-218): every appender computes its frame's CRC with
+                        common/crc32c.cc (oracle/_ref, compiled unmodified) on
+                        its own thread -- the CPU baseline of this line;
+      reference-cpu     the same reference function on the flush thread;
+      no-checksum       a no-op flush checksum: the front-end's own ceiling."""
     exe = os.path.join(REPO, "tools", "dlog_bench")
     d = tempfile.mkdtemp(prefix="dlog_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
-    threads, per = 8, 400_000
+    threads = 8
     from oracle.oracle import REF_SO, reference_available
+    workloads = [("uniform", {"per": 400_000, "lo": 42, "hi": 1024, "env": {},
+                              "what": "entry lengths uniform 42-1024 B"}),
+                 ("zipf", {"per": 25_000, "lo": 0, "hi": 0, "env": {"DLOG_ENTRY": "zipf"},
+                           "what": "entry lengths of configs[2]: Zipf 64 B - 64 KiB"})]
     engines = [("gpu", {})]
     if reference_available() and not args.no_cpu:
+        engines.append(("reference-scheme", {"REF_CRC_SO": REF_SO, "REF_SCHEME": "1"}))
         engines.append(("reference-cpu", {"REF_CRC_SO": REF_SO}))
-    # the front-end's own ceiling: the flush thread's checksum a no-op (CRCs
-    # left zero; no replay check), so appends/s is the appenders' rate alone
     engines.append(("no-checksum", {"FAKE_CRC": "1"}))
-    runs = {name: [] for name, _ in engines}
+    nruns = max(7, args.steps // 4)
+    # BENCH_DLOG_SCALE: fewer appends per run (CPU rehearsals of this leg only)
+    scale = float(os.environ.get("BENCH_DLOG_SCALE", "1"))
+    for _, w in workloads:
+        w["per"] = max(100, int(w["per"] * scale))
+    runs = {w: {e: [] for e, _ in engines} for w, _ in workloads}
     try:
-        # 5 runs per engine at the default 30 steps: a run's rate swings 1.5x with
-        # how the appenders, the flush thread and the writer share the host's
-        # cores, so the line reports the median of five
-        for _ in range(max(1, args.steps // 6)):
-            for name, extra in engines:
-                env = dict(os.environ)
-                env.update(extra)
-                progress(f"durable log run: {name}")
-                r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(per), "42", "1024"],
-                                   capture_output=True, text=True, timeout=300, env=env)
-                if r.returncode != 0:
-                    raise RuntimeError(f"dlog_bench ({name}) failed: {r.stdout[-500:]} {r.stderr[-500:]}")
-                runs[name].append(json.loads(r.stdout.strip().splitlines()[-1]))
-                shutil.rmtree(os.path.join(d, "log"), ignore_errors=True)
+        for _ in range(nruns):
+            for wname, w in workloads:
+                for name, extra in engines:
+                    env = dict(os.environ)
+                    env.update(w["env"])
+                    env.update(extra)
+                    progress(f"durable log run: {wname} / {name}")
+                    r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(w["per"]),
+                                        str(w["lo"]), str(w["hi"])],
+                                       capture_output=True, text=True, timeout=300, env=env)
+                    if r.returncode != 0:
+                        raise RuntimeError(f"dlog_bench ({wname}/{name}) failed: "
+                                           f"{r.stdout[-500:]} {r.stderr[-500:]}")
+                    runs[wname][name].append(json.loads(r.stdout.strip().splitlines()[-1]))
+                    shutil.rmtree(os.path.join(d, "log"), ignore_errors=True)
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
-    def median(rs):
+    def q(xs, p):
+        return float(np.percentile(np.asarray(xs, dtype=float), p))
+
+    def median_run(rs):
         return sorted(rs, key=lambda x: x["appends_per_s"])[(len(rs) - 1) // 2]  # (lower) median
 
     def per_flush(x):
         f = max(x["flushes"], 1)
-        return {"flushes": x["flushes"], "frame_bytes_per_flush": round(x["frame_bytes"] / f),
+        return {"flushes": x["flushes"], "host_flushes": x.get("host_flushes", 0),
+                "frame_bytes_per_flush": round(x["frame_bytes"] / f),
                 "us_per_flush": {k: round(v / f * 1e6, 2) for k, v in x["flush_s"].items()},
-                # the flush thread's checksum seconds over the whole run
-                "checksum_s": round(x["flush_s"]["batch_crc"], 4),
-                "run_s": round(x["durable_s"], 4)}
-    best = median(runs["gpu"])
-    pf = per_flush(best)
-    # the per-flush bound of the GPU batch: the round trip of a one-frame batch
-    # through the same entry point (measured by dlog_bench before its run)
-    # plus the flush's bytes at the host link's ~55 GB/s
-    pf["empty_batch_us"] = best.get("empty_batch_us", 0.0)
-    bound = pf["empty_batch_us"] + pf["frame_bytes_per_flush"] / 55e3
-    pf["batch_crc_bound_us"] = round(bound, 2)
-    pf["batch_crc_vs_bound"] = round(pf["us_per_flush"]["batch_crc"] / bound, 3)
-    # the same bound with the host link's rate as measured in the run: the
-    # incremental rate of synchronous pinned-to-device copies between the two
-    # timed sizes that bracket the flush (dlog_bench; MB-scale copies get
-    # ~32 GB/s of the link, not the 55 of 64 MiB transfers)
-    link = sorted((int(k), float(v)) for k, v in best.get("link_us", {}).items())
-    if len(link) >= 2:
+                "checksum_s": round(x["flush_s"]["batch_crc"], 4), "run_s": round(x["durable_s"], 4)}
+
+    def summary(rs):
+        ap = [x["appends_per_s"] for x in rs]
+        gb = [x["frame_GiB_per_s"] for x in rs]
+        return {"appends_per_s": {"median": round(q(ap, 50), 1), "q1": round(q(ap, 25), 1),
+                                  "q3": round(q(ap, 75), 1)},
+                "frame_gib_per_s": {"median": round(q(gb, 50), 4), "q1": round(q(gb, 25), 4),
+                                    "q3": round(q(gb, 75), 4)},
+                "durable_latency_us": {
+                    "p50_median": round(q([x["durable_latency_us"]["p50"] for x in rs], 50), 1),
+                    "p99_median": round(q([x["durable_latency_us"]["p99"] for x in rs], 50), 1)},
+                "runs": [round(v, 1) for v in ap]}
+
+    def versus(a, b):
+        """a against b: ratio of medians, and whether the IQRs separate."""
+        sa, sb = a["appends_per_s"], b["appends_per_s"]
+        verdict = ("higher" if sa["q1"] > sb["q3"] else "lower" if sa["q3"] < sb["q1"]
+                   else "within run spread")
+        ga, gb = a["frame_gib_per_s"], b["frame_gib_per_s"]
+        return {"appends_ratio": round(sa["median"] / max(sb["median"], 1e-9), 3),
+                "gib_ratio": round(ga["median"] / max(gb["median"], 1e-9), 3),
+                "beyond_spread": verdict}
+
+    out = {}
+    for wname, w in workloads:
+        eng = {name: summary(runs[wname][name]) for name, _ in engines}
+        res = {"workload": f"{threads} threads x {w['per']} appends, {w['what']}; then wait for "
+                           f"the watermark; segment files on tmpfs", "engines": eng}
+        res["gpu_vs"] = {name: versus(eng["gpu"], eng[name]) for name, _ in engines if name != "gpu"}
+        best = median_run(runs[wname]["gpu"])
+        pf = per_flush(best)
+        # the per-flush bound: the cheaper of the GPU batch's floor (a one-frame
+        # round trip through the log's entry point, measured by dlog_bench, plus
+        # the bytes at the host link's ~55 GB/s) and the flush thread's CPU
+        # path at this size (measured in the same process); the log routes
+        # each flush to one of the two by its size (durable_log.cc)
         nb = pf["frame_bytes_per_flush"]
-        i = 1
-        while i < len(link) - 1 and link[i][0] < nb:
-            i += 1
-        (n0, t0), (n1, t1) = link[i - 1], link[i]
-        rate = (n1 - n0) / max(t1 - t0, 1e-3)  # bytes per us
-        pf["link_copy_us"] = {str(k): round(v, 2) for k, v in link}
-        pf["link_rate_gb_s"] = round(rate / 1e3, 1)
-        mbound = pf["empty_batch_us"] + nb / rate
-        pf["batch_crc_bound_measured_link_us"] = round(mbound, 2)
-        pf["batch_crc_vs_measured_link"] = round(pf["us_per_flush"]["batch_crc"] / mbound, 3)
+        gpu_bound = best.get("empty_batch_us", 0.0) + nb / 55e3
+        cpu_us = _interp(best.get("cpu_batch_us", {}), nb)
+        bound = min(gpu_bound, cpu_us) if cpu_us else gpu_bound
+        pf.update({"empty_batch_us": best.get("empty_batch_us", 0.0),
+                   "gpu_batch_bound_us": round(gpu_bound, 2),
+                   "cpu_batch_us_at_flush": None if cpu_us is None else round(cpu_us, 2),
+                   "batch_crc_bound_us": round(bound, 2),
+                   "batch_crc_vs_bound": round(pf["us_per_flush"]["batch_crc"] / bound, 3)})
+        if "reference-cpu" in runs[wname]:
+            rc = per_flush(median_run(runs[wname]["reference-cpu"]))
+            pf["reference_cpu_us_per_flush"] = rc["us_per_flush"]["batch_crc"]
+            pf["reference_cpu_frame_bytes_per_flush"] = rc["frame_bytes_per_flush"]
+        res["flush"] = pf
+        if not compact:
+            res["runs_detail"] = runs[wname]
+        out[wname] = res
+    uni = out["uniform"]["engines"]
     cpu = None
-    if "reference-cpu" in runs:
-        rb = median(runs["reference-cpu"])
-        cpu = {"value": round(rb["appends_per_s"], 1), "unit": "appends/s", "cores": 1,
+    if "reference-scheme" in uni:
+        rs = uni["reference-scheme"]
+        cpu = {"value": rs["appends_per_s"]["median"], "unit": "appends/s", "cores": threads,
                "kind": "reference",
-               "sample": "the same front-end, appenders and entries, with the flush thread's "
-                         "batch checksum done by the reference common/crc32c.cc (oracle/_ref, "
-                         "compiled unmodified; crc32q dispatch) frame by frame on that thread",
-               "per_flush": per_flush(rb), "runs": runs["reference-cpu"]}
-    nc = median(runs["no-checksum"])
-    ceiling = {"appends_per_s": round(nc["appends_per_s"], 1), "per_flush": per_flush(nc),
-               "note": "same front-end with a no-op flush checksum: the appenders' own limit",
-               "runs": [round(x["appends_per_s"], 1) for x in runs["no-checksum"]]}
-    if compact:  # a leg of the default line: the per-run detail stays out
-        ceiling.pop("per_flush")
-        if cpu:
-            cpu["runs"] = [round(x["appends_per_s"], 1) for x in cpu["runs"]]
+               "sample": "the same front-end, appenders and entries (uniform 42-1024 B), with each "
+                         "appender computing its frame's CRC by the reference common/crc32c.cc "
+                         "(oracle/_ref, compiled unmodified; crc32q dispatch) on its own thread, "
+                         "as txman/durable_log.cc:215-218 does; median of the interleaved runs"}
     return {"metric": "durable-log appends/s, 8 appending threads, GPU batch CRC per flushed "
                       "segment (txman/durable_log.cc append contract)",
-            "value": round(best["appends_per_s"], 1), "unit": "appends/s", "n_gpus": 1,
-            "steps": len(runs["gpu"]), "warmup": 0, "ms_per_step": round(best["durable_s"] * 1e3, 3),
+            "value": uni["gpu"]["appends_per_s"]["median"], "unit": "appends/s", "n_gpus": 1,
+            "steps": nruns, "warmup": 0,
+            "ms_per_step": round(median_run(runs["uniform"]["gpu"])["durable_s"] * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: entry lengths uniform 42-1024 B, splitmix64 bytes",
-            "config": {"workload": f"{threads} threads x {per} appends, then wait for the "
-                                   f"watermark; segment files on tmpfs",
-                       "runs": [round(x["appends_per_s"], 1) for x in runs["gpu"]] if compact
-                       else runs["gpu"]},
-            "durable_latency_us": best["durable_latency_us"],
-            "flush": pf, "frontend_ceiling": ceiling,
-            "roofline": None, "cpu_baseline": cpu,
+            "data": "synthetic: splitmix64 entry bytes; uniform 42-1024 B and Zipf 64 B-64 KiB lengths",
+            "config": {"workload": "8 appending threads; two entry-length workloads; "
+                                   f"{nruns} interleaved runs per engine and workload"},
+            "workloads": out, "roofline": None, "cpu_baseline": cpu,
             "digest_verified": all(x["replayed"] == x["appends"] and x["replay_bad"] == 0
-                                   for name, rs in runs.items() if name != "no-checksum"
-                                   for x in rs)}
+                                   for w in runs.values() for name, rs in w.items()
+                                   if name != "no-checksum" for x in rs)}
 
 
 def run_secondary(args, E, traffic=(None, "skipped")) -> dict:

@@ -121,7 +121,9 @@ class Stats(C.Structure):
                 ("sorted_batches", C.c_uint64),
                 ("host_routed_bytes", C.c_uint64),
                 ("last_multi_devices", C.c_int32 * MAX_DEVICES),
-                ("zero_copy_batches", C.c_uint64)]
+                ("zero_copy_batches", C.c_uint64),
+                ("hint_overflows", C.c_uint64), ("host_batches", C.c_uint64),
+                ("host_batch_bytes", C.c_uint64)]
 
 _lib = None
 

@@ -235,6 +235,26 @@ int pick_devices(const int* devices, int ndev, int* out)
     return ndev > 0 ? std::min(n, ndev) : n;
 }
 
+// MI_CRC32C_CPU: the engine's CPU path by the caller's choice (host memory
+// only), counted apart from fallbacks.
+int host_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+               const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
+               unsigned flags)
+{
+    if (flags & MI_CRC32C_DEVICE)
+        return fail(MI_CRC32C_EINVAL, "MI_CRC32C_CPU takes host memory, not device pointers");
+    if (count == 0) return MI_CRC32C_OK;
+    if (!offsets || !lengths || !out) return fail(MI_CRC32C_EINVAL, "null array with count > 0");
+    for (size_t i = 0; i < count; ++i)
+        if (offsets[i] > UINT64_MAX - lengths[i])
+            return fail(MI_CRC32C_EINVAL, "record end overflows 64 bits");
+    const uint64_t total = total_bytes ? total_bytes : sum_lengths(lengths, count);
+    if (!base && total) return fail(MI_CRC32C_EINVAL, "null base");
+    mi_host::batch(base, offsets, lengths, inits, count, out);
+    mi_host::note_host_batch(total);
+    return MI_CRC32C_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -335,6 +355,8 @@ int mi_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* l
                     const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out,
                     unsigned flags)
 {
+    if (flags & MI_CRC32C_CPU)
+        return host_batch(base, offsets, lengths, inits, count, total_bytes, out, flags);
     const int st = mi_eng::batch(-1, base, offsets, lengths, inits, count, total_bytes, out, flags);
     if (st == MI_CRC32C_OK)
     {
@@ -370,6 +392,8 @@ int mi_crc32c_batch_multi(const void* base, const uint64_t* offsets, const uint3
                           uint64_t shard_min_bytes)
 {
     if (count == 0) return MI_CRC32C_OK;
+    if (flags & MI_CRC32C_CPU)
+        return host_batch(base, offsets, lengths, inits, count, total_bytes, out, flags);
     if (flags & MI_CRC32C_DEVICE)
         return fail(MI_CRC32C_EINVAL,
                     "multi-device batches take host memory: device-resident records are hashed "

@@ -2319,6 +2319,31 @@ __device__ __forceinline__ uint32_t zshift48(const uint32_t* __restrict__ pow2, 
     return v;
 }
 
+// Phase stamps of the sorted kernel (dev builds only: tools/build_variant.sh
+// TAG -DMI_SORT_STAMP=1, read by tools/sort_stamps.py through
+// mi_debug_sort_stamps): lane 0 of every wave of workgroups < 256 stores
+// s_memrealtime (100 MHz) at 8 points -- entry, cost blocks found,
+// boundaries resolved, binning pass done, first group (tables staged), team
+// groups done, lane items done, finish done.  Off in the product build.
+#ifndef MI_SORT_STAMP
+#define MI_SORT_STAMP 0
+#endif
+#if MI_SORT_STAMP
+__device__ uint64_t g_sort_stamp[256 * 16 * 8];
+#define SORT_STAMP(k)                                                                        \
+    do                                                                                       \
+    {                                                                                        \
+        if ((threadIdx.x & 63u) == 0 && blockIdx.x < 256)                                    \
+            g_sort_stamp[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (k)] =                 \
+                __builtin_amdgcn_s_memrealtime();                                            \
+    } while (0)
+#else
+#define SORT_STAMP(k) \
+    do                \
+    {                 \
+    } while (0)
+#endif
+
 template <int RB>
 __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
@@ -2345,13 +2370,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (INLOOP) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     // (1) Wave 0: the two targets and the cost blocks holding them, while the
     // other waves stage the tables (the staging's barrier covers both).
+    SORT_STAMP(0);
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
+    SORT_STAMP(1);
     // The tables are staged after the binning (step 3), which uses their LDS
     // to put the descriptors in list order first.
     constexpr uint32_t kLdsZInv = kLdsBytes + uint32_t(offsetof(SortShared, zinv));
     // (2) Exact (record, piece) boundaries of this workgroup's items.
     sort_resolve(base, off, len, count, nb, S, plog);
+    SORT_STAMP(2);
 
     // (3) Bin the items by row count, largest first.  Whole records and the
     // last pieces of split records go to this workgroup's slots of the
@@ -2432,10 +2460,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
         for (uint32_t i = 0; i < f.nf; ++i) put_full(fpos + i, desc(r, a, L, f, f.klo + i));
         if (f.last) put_last(lpos, desc(r, a, L, f, f.s.n - 1));
-        // a whole record's out[] holds its slot until the finish pass (whose
-        // record-order reads and stores are coalesced; the loop's fold value
-        // goes to wr[slot], contiguous in list order)
-        if (!INLOOP && f.last && f.s.n == 1 && !sort_is_lane(f.s, lrows)) out[r] = lpos;
     };
     uint64_t ha[CH][U];
     uint32_t hL[CH][U], hf[CH][U], hl[CH][U];
@@ -2477,6 +2501,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     pass(false);
     __syncthreads();
+    SORT_STAMP(3);
     {
         const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
         uint64_t total;
@@ -2498,6 +2523,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             if (nf > fpw || count + uint64_t(gridDim.x) * fpw > item_cap)
             {
                 ctrl[1] = 1;  // workspace too small (understated total_bytes): out[] left alone
+                ctrl[2] = 1;  // sticky: an asynchronous batch's is reported at the next stream sync
                 S.n_items = 0;
             }
             S.full_base = fb;
@@ -2545,6 +2571,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         __syncthreads();
     }
     stage_tables(tables);  // ends with a barrier
+    SORT_STAMP(4);
     // team items first, lane items (positions n_long ..) after them
     const uint32_t n_long = n_full + S.lane_base;
 
@@ -2644,59 +2671,82 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto lane_items = [&]() {
         const uint32_t n_lane = n_items - n_long;
         const uint4* const listLane = listL + n_long;
-        for (;;)
+        auto grab64 = [&]() {
+            uint32_t c = 0;
+            if (lane == 0) c = atomicAdd(&S.next_lane, 64u);
+            return uint32_t(__builtin_amdgcn_readfirstlane(int(c)));
+        };
+        auto ldesc = [&](uint32_t c) {
+            return c + lane < n_lane ? listLane[c + lane] : make_uint4(0, 0, 0, 0);
+        };
+        // Latency (round 5): a grab used to be three dependent global round
+        // trips or more (its descriptors, then its blocks four at a time,
+        // then the last block).  Now the next grab's descriptors are loaded
+        // while this grab is hashed, and all of an item's blocks are issued at
+        // once (up to 16 before the last: an item of <= 2 rows touches <= 17
+        // blocks), the last block first; they are hashed four at a time, up
+        // to the wave's largest item (the list is ordered by block count).
+        uint32_t c0 = grab64();
+        uint4 d = ldesc(c0);
+        while (c0 < n_lane)
         {
-            uint32_t c0 = 0;
-            if (lane == 0) c0 = atomicAdd(&S.next_lane, 64u);
-            c0 = uint32_t(__builtin_amdgcn_readfirstlane(int(c0)));
-            if (c0 >= n_lane) break;
+            const uint32_t c1 = grab64();
+            const uint4 d1 = ldesc(c1);
             const bool act = c0 + lane < n_lane;
-            const uint4 d = act ? listLane[c0 + lane] : make_uint4(0, 0, 0, 0);
             const uint64_t a = uint64_t(d.x) | (uint64_t(d.y) << 32);
             const uint64_t e = a + d.z;
             const uint32_t q = uint32_t(a) & 15u;
             const int32_t K = act ? int32_t(((e + 15) >> 4) - (a >> 4)) : 0;  // blocks, >= 1
             const uint32_t t = ((uint32_t(e) - 1u) & 15u) + 1u;                // item bytes' end in the last block
             const uint32_t rec = d.w & kSortRecMask;
+            const uint8_t* const pb = reinterpret_cast<const uint8_t*>(a & ~uint64_t(15));
+            const int32_t nb = K - 1;  // blocks before the last
+            uint4 xl = load16_edge(act ? pb + 16 * (K - 1) : zero16);
             const bool with_init = !(d.w & kSortMulti) || (d.w & kSortFirst);
             const uint32_t ninit = !with_init ? 0u : inits ? (act ? ~inits[rec] : 0u) : 0xFFFFFFFFu;
             const uint64_t shi = uint64_t(ninit) << ((q & 3u) * 8u);
-            const uint32_t xl = uint32_t(shi), xh = uint32_t(shi >> 32);
+            const uint32_t xlo = uint32_t(shi), xhi = uint32_t(shi >> 32);
             const uint32_t qd = q >> 2;
-            const uint4 xf = make_uint4(qd == 0 ? xl : 0u, qd == 1 ? xl : qd == 0 ? xh : 0u,
-                                        qd == 2 ? xl : qd == 1 ? xh : 0u, qd == 3 ? xl : qd == 2 ? xh : 0u);
-            const uint32_t xs = qd == 3 ? xh : 0u;  // the init word's spill into block 1
+            const uint4 xf = make_uint4(qd == 0 ? xlo : 0u, qd == 1 ? xlo : qd == 0 ? xhi : 0u,
+                                        qd == 2 ? xlo : qd == 1 ? xhi : 0u, qd == 3 ? xlo : qd == 2 ? xhi : 0u);
+            const uint32_t xs = qd == 3 ? xhi : 0u;  // the init word's spill into block 1
             const uint4 kf = make_uint4(keep_from(int32_t(q), 0), keep_from(int32_t(q), 1),
                                         keep_from(int32_t(q), 2), keep_from(int32_t(q), 3));
-            const uint8_t* const pb = reinterpret_cast<const uint8_t*>(a & ~uint64_t(15));
-            const int32_t nb = K - 1;  // blocks before the last
             uint32_t st = 0;
-            // four blocks per step, all loads first
-            for (int32_t j = 0; __builtin_amdgcn_ballot_w64(j < nb) != 0; j += 4)
+            for (int32_t j = 0; __builtin_amdgcn_ballot_w64(j < nb) != 0; j += 16)
             {
-                uint4 w[4];
+                uint4 w[16];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    w[u] = load16_edge(j + u < nb ? pb + 16 * (j + u) : zero16);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
+                for (int u = 0; u < 16; ++u)
                 {
-                    uint4 x = w[u];
-                    if (j + u == 0)
+                    w[u] = make_uint4(0, 0, 0, 0);
+                    if (__builtin_amdgcn_ballot_w64(j + u < nb) != 0)  // wave-uniform
+                        w[u] = load16_edge(j + u < nb ? pb + 16 * (j + u) : zero16);
+                }
+#pragma unroll
+                for (int u4 = 0; u4 < 16; u4 += 4)
+                {
+                    if (__builtin_amdgcn_ballot_w64(j + u4 < nb) == 0) break;
+#pragma unroll
+                    for (int u = u4; u < u4 + 4; ++u)
                     {
-                        x.x = __builtin_amdgcn_bitop3_b32(x.x, kf.x, xf.x, 0x6A);
-                        x.y = __builtin_amdgcn_bitop3_b32(x.y, kf.y, xf.y, 0x6A);
-                        x.z = __builtin_amdgcn_bitop3_b32(x.z, kf.z, xf.z, 0x6A);
-                        x.w = __builtin_amdgcn_bitop3_b32(x.w, kf.w, xf.w, 0x6A);
+                        uint4 x = w[u];
+                        if (j + u == 0)
+                        {
+                            x.x = __builtin_amdgcn_bitop3_b32(x.x, kf.x, xf.x, 0x6A);
+                            x.y = __builtin_amdgcn_bitop3_b32(x.y, kf.y, xf.y, 0x6A);
+                            x.z = __builtin_amdgcn_bitop3_b32(x.z, kf.z, xf.z, 0x6A);
+                            x.w = __builtin_amdgcn_bitop3_b32(x.w, kf.w, xf.w, 0x6A);
+                        }
+                        if (j + u == 1) x.x ^= xs;
+                        const uint32_t sn = zT<4>(st ^ x.x) ^ zT<3>(x.y) ^ zT<2>(x.z) ^ zT<1>(x.w);
+                        st = j + u < nb ? sn : st;
                     }
-                    if (j + u == 1) x.x ^= xs;
-                    const uint32_t sn = zT<4>(st ^ x.x) ^ zT<3>(x.y) ^ zT<2>(x.z) ^ zT<1>(x.w);
-                    st = j + u < nb ? sn : st;
                 }
             }
             // the last block: bytes >= t zeroed, then the t-byte step
             {
-                uint4 x = load16_edge(act ? pb + 16 * (K - 1) : zero16);
+                uint4 x = xl;
                 const bool first = K == 1;
                 x.x = first ? __builtin_amdgcn_bitop3_b32(x.x, kf.x, xf.x, 0x6A) : x.x;
                 x.y = first ? __builtin_amdgcn_bitop3_b32(x.y, kf.y, xf.y, 0x6A) : x.y;
@@ -2719,6 +2769,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            c0 = c1;
+            d = d1;
         }
     };
     uint32_t g_cur = grab();
@@ -2888,45 +2940,41 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     flush();
 
+    SORT_STAMP(5);
     lane_items();
+    SORT_STAMP(6);
     if (INLOOP) return;  // whole records were finished in the loop
-    // Finish pass, in record order: a whole record's fold value (wr at its
-    // slot) is Z_m(raw) of its bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).
-    // (Split records were finished by their pieces' XORs.)
+    // Finish pass, in list order (round 5): a whole record's fold value W
+    // (wr at its slot, eight consecutive words per group) is Z_m(raw) of its
+    // bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).  The team items past the
+    // full pieces -- whole records and the heads of split records, which
+    // their XORs finished -- sit at list positions n_full .. n_long - 1: their
+    // descriptors at items[rlo + k] and their fold values at wr[rlo + k],
+    // both read in order, together (rounds 3-4 read off[], len[] and the slot
+    // left in out[r] in record order, then wr[slot]: two dependent round
+    // trips, and the binning pass stored every slot).  The CRCs go to out[rec],
+    // scattered inside the workgroup's record range.
     S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     __syncthreads();  // the workgroup's own stores are visible to it past the barrier
-    // four records per thread per round: every load of the round issued
-    // before any is used (the pass is two dependent global round trips and
-    // five LDS rounds per record; round 3 A/B: -1 to -2 us against one record
-    // per round, profiles/r03_sorted_late_finish_ab.txt)
     constexpr uint32_t FU = 4;
-    for (uint64_t r0 = uint64_t(rlo) + threadIdx.x; r0 < rend; r0 += FU * kBlock)
+    const uint32_t n_whole = n_long - n_full;
+    const uint4* const dl = items + rlo;
+    for (uint32_t k0 = threadIdx.x; k0 < n_whole; k0 += FU * kBlock)
     {
-        uint64_t av[FU];
-        uint32_t Lv[FU], sv[FU];
-#pragma unroll
-        for (uint32_t u = 0; u < FU; ++u)
-        {
-            const uint64_t r = r0 + u * kBlock;
-            const bool in = r < rend;
-            av[u] = uint64_t(base) + (in ? off[r] : 0);
-            Lv[u] = in ? len[r] : 0u;
-            sv[u] = in ? out[r] : 0u;
-        }
+        uint4 dv[FU];
         uint32_t wv[FU];
-        bool own[FU];
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
         {
-            const uint64_t r = r0 + u * kBlock;
-            const RecInfo f = info(r, av[u], Lv[u]);
-            own[u] = r < rend && f.s.n == 1 && f.last && !sort_is_lane(f.s, lrows);
-            wv[u] = own[u] ? wr[uint64_t(rlo) + sv[u]] : 0u;
+            const uint32_t k = k0 + u * kBlock;
+            dv[u] = k < n_whole ? dl[k] : make_uint4(0, 0, 0, kSortMulti);
+            wv[u] = k < n_whole ? wr[uint64_t(rlo) + k] : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
         {
-            const uint32_t m = uint32_t(0u - uint32_t(av[u] + Lv[u])) & 127u;
+            const uint64_t ps = uint64_t(dv[u].x) | (uint64_t(dv[u].y) << 32);
+            const uint32_t m = uint32_t(0u - uint32_t(ps + dv[u].z)) & 127u;
             uint32_t v = wv[u];
             const uint32_t n = 128u - m;
             uint32_t t = zT_n(v, n & 15u);
@@ -2935,10 +2983,19 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             t = (n & 64u) ? zG(kLdsZ64, t) : t;
             t = zG(kLdsZInv, t);
             v = m ? t : v;
-            if (own[u]) out[r0 + u * kBlock] = ~v;
+            if (!(dv[u].w & kSortMulti)) out[dv[u].w & kSortRecMask] = ~v;
         }
     }
+    SORT_STAMP(7);
 }
+
+#if MI_SORT_STAMP
+extern "C" __attribute__((visibility("default"))) int mi_debug_sort_stamps(uint64_t* host, size_t n)
+{
+    n = n < sizeof(g_sort_stamp) / 8 ? n : sizeof(g_sort_stamp) / 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_stamp), n * 8) == hipSuccess ? 0 : -5;
+}
+#endif
 
 // Slots for one workgroup's full pieces: items whose cost starts in its share
 // (at most C (1000 + w) / (1000 G) + 1, the XCD-weighted share) are at least

@@ -87,6 +87,20 @@ int gpu_batch(void* ctx, const void* base, const uint64_t* off, const uint32_t* 
 // rather than inside a batch, whose lengths are 32-bit.
 constexpr uint64_t kBatchFrameMax = uint64_t(1) << 30;
 
+// Flushes below this many frame bytes are checksummed on the flush thread's
+// CPU (the engine's crc32q loop, MI_CRC32C_CPU): the GPU batch's floor (a
+// launch, zero-copy reads over PCIe and the completion word, ~11-12 us) costs
+// more there than the CPU loop's ~13 GB/s.  The crossover measured per flush
+// size with tools/flush_probe.
+constexpr uint64_t kHostBatchMaxDefault = uint64_t(384) << 10;
+
+uint64_t host_batch_max(const consus::durable_log_options& o)
+{
+    if (const char* e = std::getenv("MI_DLOG_HOST_BATCH_MAX"))
+        return std::strtoull(e, nullptr, 10);
+    return o.host_batch_max < 0 ? kHostBatchMaxDefault : uint64_t(o.host_batch_max);
+}
+
 bool pwrite_all(int fd, const unsigned char* p, size_t n, off_t off)
 {
     while (n)
@@ -364,6 +378,10 @@ durable_log::durable_log(const durable_log_options& options)
     , m_flush_idle(false)
     , m_crc(gpu_batch)
     , m_crc_ctx(&m_opts)
+    , m_host_max(host_batch_max(options))
+    , m_host_flushes(0)
+    , m_append_crc(nullptr)
+    , m_ext_malloc_fail(false)
     , m_pinned(true)
     , m_flushes(0)
     , m_frames_flushed(0)
@@ -431,6 +449,17 @@ void durable_log::set_batch_crc_for_testing(durable_log_batch_crc fn, void* ctx)
     m_crc_ctx = fn ? ctx : &m_opts;
     m_pinned = !fn;
 }
+
+void durable_log::set_append_crc_for_testing(uint32_t (*fn)(uint32_t, const unsigned char*, size_t))
+{
+    std::lock_guard<std::mutex> hold(m_mtx);
+    if (m_opened) return;
+    m_append_crc = fn;
+}
+
+void durable_log::set_external_malloc_failure_for_testing(bool fail) { m_ext_malloc_fail = fail; }
+
+uint64_t durable_log::host_flushes() const { return m_host_flushes; }
 
 uint64_t durable_log::flushes() const { return m_flushes; }
 uint64_t durable_log::frames_flushed() const { return m_frames_flushed; }
@@ -685,13 +714,17 @@ int64_t durable_log::append(const unsigned char* entry, size_t entry_sz)
                 }
                 // encode_header (txman/durable_log.cc:57-61) and the entry
                 const uint64_t recno = seg->base + idx;
-                unsigned char* p = external ? static_cast<unsigned char*>(malloc(frame))
-                                            : seg->arena + at;
+                unsigned char* p = !external ? seg->arena + at
+                                   : m_ext_malloc_fail.load() ? nullptr
+                                   : static_cast<unsigned char*>(malloc(frame));
                 if (p)
                 {
                     pack64be(recno, p);
                     pack64be(entry_sz, p + 8);
                     if (entry_sz) memcpy(p + kHeader, entry, entry_sz);
+                    // the reference scheme (bench hook): this thread's CRC
+                    if (m_append_crc)
+                        pack32be(m_append_crc(0, p, kHeader + entry_sz), p + kHeader + entry_sz);
                 }
                 if (external)
                 {
@@ -852,6 +885,13 @@ void durable_log::release_external(uint64_t bytes)
 int durable_log::batch_crc(const unsigned char* base, const uint64_t* offs, const uint32_t* lens,
                            size_t n, uint64_t total, uint32_t* out)
 {
+    // below the GPU/CPU crossover: the flush thread's CPU (counted)
+    if (m_crc == gpu_batch && total < m_host_max &&
+        mi_crc32c_batch(base, offs, lens, nullptr, n, total, out, MI_CRC32C_CPU) == MI_CRC32C_OK)
+    {
+        m_host_flushes.fetch_add(1, std::memory_order_relaxed);
+        return 0;
+    }
     if (m_crc(m_crc_ctx, base, offs, lens, n, total, out) == 0) return 0;
     mi_host::batch(base, offs, lens, nullptr, n, out);
     mi_host::note_fallback(MI_CRC32C_EHIP, total);
@@ -936,13 +976,17 @@ int durable_log::prepare_segment(segment* seg, uint64_t& n, uint64_t& used, writ
             total += m_lens[i];
         }
         lap(1);
-        if (k) batch_crc(seg->arena, m_offs.data(), m_lens.data(), size_t(k), total, m_crcs.data());
-        for (segment::External& x : ext)
-            pack32be(frame_crc(x.frame, x.bytes - kTrailer), x.frame + x.bytes - kTrailer);
+        // (with the append-CRC bench hook every frame already holds its CRC)
+        if (k && !m_append_crc)
+            batch_crc(seg->arena, m_offs.data(), m_lens.data(), size_t(k), total, m_crcs.data());
+        if (!m_append_crc)
+            for (segment::External& x : ext)
+                pack32be(frame_crc(x.frame, x.bytes - kTrailer), x.frame + x.bytes - kTrailer);
         lap(2);
         // crc32c(crc32c(0, header, 16), entry) == crc32c(0, header || entry),
         // stored big-endian after the entry (txman/durable_log.cc:215-224)
-        for (uint64_t i = 0; i < k; ++i) pack32be(m_crcs[i], seg->arena + m_offs[i] + m_lens[i]);
+        if (!m_append_crc)
+            for (uint64_t i = 0; i < k; ++i) pack32be(m_crcs[i], seg->arena + m_offs[i] + m_lens[i]);
         lap(3);
     }
     uint64_t bytes = used;
@@ -1325,6 +1369,26 @@ int64_t mi_dlog_replay(mi_dlog* l, void (*f)(void*, const unsigned char*, size_t
     return l->log.replay(f, p);
 }
 uint64_t mi_dlog_flushes(mi_dlog* l) { return l->log.flushes(); }
+uint64_t mi_dlog_host_flushes(mi_dlog* l) { return l->log.host_flushes(); }
+mi_dlog* mi_dlog_create_opts(size_t segment_capacity, int gpus, uint64_t shard_min_bytes,
+                             int64_t host_batch_max)
+{
+    consus::durable_log_options o;
+    o.segment_capacity = segment_capacity;
+    o.gpus = gpus;
+    o.shard_min_bytes = shard_min_bytes;
+    o.host_batch_max = host_batch_max;
+    return new mi_dlog(o);
+}
+void mi_dlog_set_append_crc_for_testing(mi_dlog* l,
+                                        uint32_t (*fn)(uint32_t, const unsigned char*, size_t))
+{
+    l->log.set_append_crc_for_testing(fn);
+}
+void mi_dlog_set_external_malloc_failure_for_testing(mi_dlog* l, int fail)
+{
+    l->log.set_external_malloc_failure_for_testing(fail != 0);
+}
 uint64_t mi_dlog_frames_flushed(mi_dlog* l) { return l->log.frames_flushed(); }
 uint64_t mi_dlog_external_peak(mi_dlog* l) { return l->log.external_bytes_peak(); }
 void mi_dlog_flush_seconds(mi_dlog* l, double out[6]) { l->log.flush_seconds(out); }

@@ -337,6 +337,9 @@ struct Ctx
     // size hint was too small (sorted path: ctrl[1] != 0; piece path: the
     // plan's item total > plan_cap)
     uint32_t* sorted_ctrl = nullptr;
+    // an asynchronous sorted batch ran since the last stream sync: its
+    // overflow (understated size hint) sits in the sticky ctrl[2]
+    bool async_sorted_unchecked = false;
     uint32_t* plan_total = nullptr;
     uint64_t plan_cap = 0;
 
@@ -498,9 +501,13 @@ const uint8_t* mapped_device_ptr(const void* p)
 // Checking the first byte alone let a span that runs from a mapped buffer
 // into pageable memory reach the kernel, which would then read past the
 // mapping.  Both ends must be mapped, at device addresses the
-// same distance apart; when the runtime reports the device allocation's
-// range, the span must lie inside it too (tools/zc_probe.py:
-// profiles/r04_zero_copy_pointer_probe.txt).
+// same distance apart, and the span must lie inside ONE device allocation:
+// when the runtime reports the allocation's range, that range bounds it;
+// when it does not -- hipHostRegister'ed memory, for which ROCm 7.2 reports
+// the size with a null base (tools/zc_probe.py:
+// profiles/r04_zero_copy_pointer_probe.txt) -- two registered regions with a
+// pageable gap between them would pass the two-end check, so every page of
+// the span is checked instead.
 const uint8_t* mapped_span_device_ptr(const uint8_t* p, uint64_t n)
 {
     const uint8_t* d0 = mapped_device_ptr(p);
@@ -509,15 +516,21 @@ const uint8_t* mapped_span_device_ptr(const uint8_t* p, uint64_t n)
     if (!d1 || d1 < d0 || uint64_t(d1 - d0) != n - 1) return nullptr;
     hipDeviceptr_t pbase = nullptr;
     size_t psize = 0;
-    // (for hipHostRegister'ed memory ROCm 7.2 reports the size with a null
-    // base: then the two-point check stands alone)
     if (hipMemGetAddressRange(&pbase, &psize, const_cast<uint8_t*>(d0)) == hipSuccess && pbase)
     {
         const uint8_t* b = static_cast<const uint8_t*>(pbase);
-        if (d0 < b || uint64_t(d1 - b) >= psize) return nullptr;
+        return d0 < b || uint64_t(d1 - b) >= psize ? nullptr : d0;
     }
-    else
-        (void)hipGetLastError();
+    (void)hipGetLastError();
+    // no allocation range: every page between the two ends, mapped at the
+    // same distance
+    constexpr uint64_t kPage = 4096;
+    const uintptr_t first = (reinterpret_cast<uintptr_t>(p) | (kPage - 1)) + 1;
+    for (uintptr_t q = first; q < reinterpret_cast<uintptr_t>(p) + n; q += kPage)
+    {
+        const uint8_t* dq = mapped_device_ptr(reinterpret_cast<const uint8_t*>(q));
+        if (dq != d0 + (q - reinterpret_cast<uintptr_t>(p))) return nullptr;
+    }
     return d0;
 }
 
@@ -802,6 +815,25 @@ int mi_crc32c_stream_sync(void)
     Ctx* c = thread_ctx(&st);
     if (!c) return st;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->async_sorted_unchecked)
+    {
+        // an asynchronous sorted batch whose total_bytes hint
+        // understated its records left out[] incomplete (no access went out
+        // of bounds); the kernel's sticky word says so, read and cleared here
+        c->async_sorted_unchecked = false;
+        uint32_t* w = c->pin_small.as<uint32_t>() + 2;
+        HIP_TRY(hipMemcpyAsync(w, c->srt_ctrl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (*w)
+        {
+            HIP_TRY(hipMemsetAsync(c->srt_ctrl.as<uint32_t>() + 2, 0, 4, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            mi_host::note_hint_overflow();
+            return fail(MI_CRC32C_EINVAL,
+                        "an asynchronous batch's total_bytes hint understated the sum of its "
+                        "lengths: its out[] is incomplete");
+        }
+    }
     return MI_CRC32C_OK;
 }
 
@@ -854,6 +886,7 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         c->sorted_ctrl = c->plan_total = nullptr;
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out)))
             return st;
+        if (flags & MI_CRC32C_ASYNC) c->async_sorted_unchecked |= c->sorted_ctrl != nullptr;
         if ((flags & MI_CRC32C_ASYNC) || (!c->sorted_ctrl && !c->plan_total))
             return finish(c, flags);
         // Synchronous batch sized by the caller's hint: if the hint understated
@@ -867,6 +900,12 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         HIP_TRY(hipStreamSynchronize(c->stream));
         const bool overflow = c->sorted_ctrl ? *flag != 0 : *flag > c->plan_cap;
         if (!overflow) return MI_CRC32C_OK;
+        // the sticky word (ctrl[2]) is for asynchronous batches: this one is
+        // recovered here.  With an unchecked asynchronous batch before it on
+        // the stream the word may be that batch's too, so it stays for the
+        // next stream sync to report (conservatively).
+        if (c->sorted_ctrl && !c->async_sorted_unchecked)
+            HIP_TRY(hipMemsetAsync(c->sorted_ctrl + 2, 0, 4, c->stream));
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, 0, out))) return st;
         return finish(c, flags);
     }

@@ -68,7 +68,8 @@ bool have_sse42()
 #endif
 
 std::atomic<uint64_t> g_gpu_calls{0}, g_fb_calls{0}, g_fb_bytes{0}, g_sharded{0}, g_sorted{0},
-    g_routed_calls{0}, g_routed_bytes{0}, g_zero_copy{0};
+    g_routed_calls{0}, g_routed_bytes{0}, g_zero_copy{0}, g_hint_overflow{0},
+    g_host_batches{0}, g_host_batch_bytes{0};
 std::atomic<int> g_fb_status{0};
 std::atomic<int> g_multi_ranges{0};
 std::atomic<int> g_multi_devs[MI_CRC32C_MAX_DEVICES];
@@ -112,6 +113,12 @@ void note_gpu_call() { g_gpu_calls.fetch_add(1, std::memory_order_relaxed); }
 void note_sharded_call() { g_sharded.fetch_add(1, std::memory_order_relaxed); }
 void note_sorted_batch() { g_sorted.fetch_add(1, std::memory_order_relaxed); }
 void note_zero_copy_batch() { g_zero_copy.fetch_add(1, std::memory_order_relaxed); }
+void note_hint_overflow() { g_hint_overflow.fetch_add(1, std::memory_order_relaxed); }
+void note_host_batch(uint64_t bytes)
+{
+    g_host_batches.fetch_add(1, std::memory_order_relaxed);
+    g_host_batch_bytes.fetch_add(bytes, std::memory_order_relaxed);
+}
 void note_host_routed(uint64_t bytes)
 {
     g_routed_calls.fetch_add(1, std::memory_order_relaxed);
@@ -139,6 +146,9 @@ void mi_crc32c_stats(mi_crc32c_stats_t* out)
     out->host_routed_bytes = mi_host::g_routed_bytes.load();
     out->sorted_batches = mi_host::g_sorted.load();
     out->zero_copy_batches = mi_host::g_zero_copy.load();
+    out->hint_overflows = mi_host::g_hint_overflow.load();
+    out->host_batches = mi_host::g_host_batches.load();
+    out->host_batch_bytes = mi_host::g_host_batch_bytes.load();
     out->last_fallback_status = mi_host::g_fb_status.load();
     const int ranges = mi_host::g_multi_ranges.load();
     out->last_multi_ranges = ranges;
@@ -154,6 +164,9 @@ void mi_crc32c_stats_reset(void)
     mi_host::g_sharded.store(0);
     mi_host::g_sorted.store(0);
     mi_host::g_zero_copy.store(0);
+    mi_host::g_hint_overflow.store(0);
+    mi_host::g_host_batches.store(0);
+    mi_host::g_host_batch_bytes.store(0);
     mi_host::g_routed_calls.store(0);
     mi_host::g_routed_bytes.store(0);
     mi_host::g_fb_status.store(0);

@@ -32,6 +32,8 @@ void note_gpu_call();
 void note_sharded_call();
 void note_sorted_batch();
 void note_zero_copy_batch();
+void note_hint_overflow();
+void note_host_batch(uint64_t bytes);
 void note_host_routed(uint64_t bytes);
 void note_multi(int ranges, const int* devices);
 

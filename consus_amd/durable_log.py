@@ -18,6 +18,10 @@ BATCH_CRC_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void
 _SIGS = {
     "mi_dlog_create": (C.c_void_p, [C.c_size_t]),
     "mi_dlog_create_ex": (C.c_void_p, [C.c_size_t, C.c_int, C.c_uint64]),
+    "mi_dlog_create_opts": (C.c_void_p, [C.c_size_t, C.c_int, C.c_uint64, C.c_int64]),
+    "mi_dlog_host_flushes": (C.c_uint64, [C.c_void_p]),
+    "mi_dlog_set_append_crc_for_testing": (None, [C.c_void_p, C.c_void_p]),
+    "mi_dlog_set_external_malloc_failure_for_testing": (None, [C.c_void_p, C.c_int]),
     "mi_dlog_destroy": (None, [C.c_void_p]),
     "mi_dlog_open": (C.c_int, [C.c_void_p, C.c_char_p]),
     "mi_dlog_close": (None, [C.c_void_p]),
@@ -53,12 +57,14 @@ def _lib():
 
 class DurableLog:
     def __init__(self, segment_capacity: int = 0, batch_crc=None, gpus: int = 0,
-                 shard_min: int = 0):
+                 shard_min: int = 0, host_batch_max: int = -1):
         """batch_crc: optional C function pointer (mi_dlog_batch_crc) used
         instead of the GPU -- a test hook; must be set before open().
-        gpus / shard_min: consus::durable_log_options (devices one flush may
-        shard over, 0 = all usable; per-device share threshold, 0 = default)."""
-        self._h = _lib().mi_dlog_create_ex(segment_capacity, gpus, shard_min)
+        gpus / shard_min / host_batch_max: consus::durable_log_options
+        (devices one flush may shard over, 0 = all usable; per-device share
+        threshold, 0 = default; flushes below host_batch_max bytes on the
+        CPU, -1 = the measured crossover, 0 = never)."""
+        self._h = _lib().mi_dlog_create_opts(segment_capacity, gpus, shard_min, host_batch_max)
         self._keep = batch_crc
         if batch_crc is not None:
             _lib().mi_dlog_set_batch_crc_for_testing(self._h, C.cast(batch_crc, C.c_void_p), None)
@@ -98,6 +104,13 @@ class DurableLog:
 
     def flushes(self) -> int:
         return int(_lib().mi_dlog_flushes(self._h))
+
+    def host_flushes(self) -> int:
+        """Flushes checksummed on the flush thread's CPU (below host_batch_max)."""
+        return int(_lib().mi_dlog_host_flushes(self._h))
+
+    def set_external_malloc_failure_for_testing(self, fail: bool) -> None:
+        _lib().mi_dlog_set_external_malloc_failure_for_testing(self._h, int(bool(fail)))
 
     def frames_flushed(self) -> int:
         return int(_lib().mi_dlog_frames_flushed(self._h))

@@ -52,6 +52,11 @@ extern "C" {
                                    call on the engine's CPU path (counted in
                                    mi_crc32c_stats) instead of returning the failure.
                                    Bad arguments (MI_CRC32C_EINVAL) still fail. */
+#define MI_CRC32C_CPU 0x10u     /* mi_crc32c_batch[_multi] on host memory: hash on the
+                                   engine's CPU path (crc32q) by the caller's choice, no
+                                   GPU involved -- the durable log sends flushes below its
+                                   measured GPU/CPU crossover this way (counted in
+                                   host_batches / host_batch_bytes, not as a fallback) */
 
 /* ---- engine ------------------------------------------------------------- */
 /* Select the device and upload the operator tables.  Idempotent; called
@@ -91,6 +96,13 @@ typedef struct mi_crc32c_stats_t
                                      last multi-device call, in range order (-1: unused) */
     uint64_t zero_copy_batches;   /* host batches the kernels read in place from mapped
                                      pinned memory (mi_host_malloc_pinned) */
+    uint64_t hint_overflows;      /* asynchronous device batches whose total_bytes hint
+                                     understated their records (reported by the next
+                                     mi_crc32c_stream_sync, which then fails) */
+    uint64_t host_batches;        /* batches hashed on the CPU path by the caller's choice
+                                     (MI_CRC32C_CPU: durable-log flushes below the
+                                     crossover) */
+    uint64_t host_batch_bytes;    /* bytes of those batches */
 } mi_crc32c_stats_t;
 void mi_crc32c_stats(mi_crc32c_stats_t* out);
 void mi_crc32c_stats_reset(void);

@@ -26,6 +26,11 @@ mi_dlog* mi_dlog_create(size_t segment_capacity);
  * only); shard_min_bytes = per-device share below which a flush uses fewer
  * devices (0 = the engine's measured default). */
 mi_dlog* mi_dlog_create_ex(size_t segment_capacity, int gpus, uint64_t shard_min_bytes);
+/* The same plus host_batch_max: a flush whose frames total fewer bytes is
+ * checksummed on the flush thread's CPU (-1 = the measured GPU/CPU crossover,
+ * 0 = never; MI_DLOG_HOST_BATCH_MAX in the environment overrides). */
+mi_dlog* mi_dlog_create_opts(size_t segment_capacity, int gpus, uint64_t shard_min_bytes,
+                             int64_t host_batch_max);
 void mi_dlog_destroy(mi_dlog* log);
 int mi_dlog_open(mi_dlog* log, const char* dir);           /* 1 = ok, 0 = failed (bool) */
 void mi_dlog_close(mi_dlog* log);
@@ -36,6 +41,8 @@ void mi_dlog_wake(mi_dlog* log);
 int mi_dlog_error(mi_dlog* log);
 int64_t mi_dlog_replay(mi_dlog* log, void (*f)(void*, const unsigned char*, size_t), void* p);
 uint64_t mi_dlog_flushes(mi_dlog* log);
+/* flushes checksummed on the flush thread's CPU (below host_batch_max) */
+uint64_t mi_dlog_host_flushes(mi_dlog* log);
 uint64_t mi_dlog_frames_flushed(mi_dlog* log);
 /* most bytes of oversized frames (more than half a segment, staged outside
  * the arenas) held at once: bounded by max(2 x segment capacity, 16 MiB,
@@ -61,6 +68,14 @@ void mi_dlog_set_fsync_delay_for_testing(mi_dlog* log, uint32_t microseconds);
  * reservation (segment sealed or full), before waiting for the switch. */
 void mi_dlog_set_append_hook_for_testing(mi_dlog* log, void (*fn)(void* ctx, int point),
                                          void* ctx);
+/* Bench hook (call before open): the reference's checksum placement
+ * (txman/durable_log.cc:215-218) -- each appender computes its frame's CRC
+ * with fn(0, header || entry, 16 + entry_sz) on its own thread; the flush
+ * thread checksums nothing. */
+void mi_dlog_set_append_crc_for_testing(mi_dlog* log,
+                                        uint32_t (*fn)(uint32_t, const unsigned char*, size_t));
+/* Test hook: the staging malloc of an oversized frame fails (ENOMEM). */
+void mi_dlog_set_external_malloc_failure_for_testing(mi_dlog* log, int fail);
 /* One line of internal state for watchdogs (flush-thread phase, the active
  * segment's reservation word, staged / failed frames, queued jobs, appenders
  * waiting for a segment switch); at most n bytes including the NUL. */

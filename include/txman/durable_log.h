@@ -62,6 +62,11 @@ struct durable_log_options
                                    // gfx950 device, 1 = the engine's default device only
     uint64_t shard_min_bytes = 0;  // per-device share below which a flush stays on fewer
                                    // devices; 0 = the engine's measured default (4 MiB)
+    int64_t host_batch_max = -1;   // a flush whose frames total fewer bytes is checksummed
+                                   // on the flush thread's CPU (crc32q, MI_CRC32C_CPU):
+                                   // -1 = the measured GPU/CPU crossover
+                                   // (kHostBatchMaxDefault in durable_log.cc), 0 = never;
+                                   // the environment's MI_DLOG_HOST_BATCH_MAX overrides
 };
 
 // As in the reference, the class sits in Consus's hidden-visibility namespace
@@ -112,6 +117,17 @@ class __attribute__((visibility("default"))) durable_log
         // to switch segments.  A test parks one appender there while the
         // flush thread switches segments under it.
         void set_append_hook_for_testing(void (*fn)(void* ctx, int point), void* ctx);
+        // Bench hook (call before open): the reference's checksum placement
+        // (txman/durable_log.cc:215-218) -- every appender computes its
+        // frame's CRC with fn(0, header || entry) on its own thread, outside
+        // any lock, and stores it in the frame; the flush thread then
+        // checksums nothing.  bench.py's durable-log leg times the reference
+        // common/crc32c.cc this way beside the batch engines.
+        void set_append_crc_for_testing(uint32_t (*fn)(uint32_t, const unsigned char*, size_t));
+        // Test hook: the staging malloc of an oversized frame fails (ENOMEM).
+        void set_external_malloc_failure_for_testing(bool fail);
+        // Flushes checksummed on the flush thread's CPU (below host_batch_max).
+        uint64_t host_flushes() const;
         // One line of the log's internal state (flush-thread phase, the
         // active segment's reservation word, queued jobs, appenders waiting
         // for a switch) for watchdogs; writes at most n bytes, NUL included.
@@ -170,6 +186,10 @@ class __attribute__((visibility("default"))) durable_log
         std::atomic<bool> m_flush_idle;      // the flush thread sleeps for a first frame
         durable_log_batch_crc m_crc;
         void* m_crc_ctx;
+        uint64_t m_host_max;                 // flushes below this many bytes: the CPU path
+        std::atomic<uint64_t> m_host_flushes;
+        uint32_t (*m_append_crc)(uint32_t, const unsigned char*, size_t);  // bench hook
+        std::atomic<bool> m_ext_malloc_fail;  // test hook
         bool m_pinned;
         std::atomic<uint64_t> m_flushes;
         std::atomic<uint64_t> m_frames_flushed;

@@ -18,6 +18,10 @@ if REPO not in sys.path:
 # the GPU tests certify the HIP kernels.  tests/test_routing.py turns it on
 # where it tests it.
 os.environ["MI_CRC32C_GPU_MIN"] = "0"
+# Likewise the durable log's flush routing (durable_log_options::host_batch_max):
+# every flush of the suite is checksummed by the GPU batch;
+# tests/test_durable_log.py::test_small_flushes_route_to_the_cpu turns it on.
+os.environ["MI_DLOG_HOST_BATCH_MAX"] = "0"
 
 
 def pytest_configure(config):

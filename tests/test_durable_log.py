@@ -407,8 +407,9 @@ def test_slow_fsync_overlaps_next_write(make_log, tmp_path):
 
 
 def test_watermark_never_passes_a_failed_record(make_log, tmp_path):
-    """an append whose staging malloc fails (an entry larger than
-    the address space) puts the log into ENOMEM.  As in the reference, whose
+    """an append whose staging malloc fails puts the log into
+    ENOMEM (the failure is injected by a test hook on an oversized frame's
+    staging malloc, ADVICE r4: no real allocation is attempted).  As in the reference, whose
     flush thread stops at the first error (txman/durable_log.cc:226-230,
     287-347), segments not yet fsynced are then dropped: the watermark never
     passes the failed record, later appends fail, and the files hold a
@@ -425,7 +426,11 @@ def test_watermark_never_passes_a_failed_record(make_log, tmp_path):
     wait_durable(log, 50)
     for i, e in enumerate(entries[50:]):
         assert log.append(e) == 51 + i
-    assert _lib().mi_dlog_append(log._h, b"x", 1 << 50) == -1
+    # an entry of more than half the 64 KiB staging buffer is staged on its
+    # own: its (injected) malloc failure is fatal for the log
+    big = bytes(40000)
+    log.set_external_malloc_failure_for_testing(True)
+    assert _lib().mi_dlog_append(log._h, big, len(big)) == -1
     assert log.error() == errno.ENOMEM
     t0 = time.time()
     while time.time() - t0 < 0.3:
@@ -436,3 +441,81 @@ def test_watermark_never_passes_a_failed_record(make_log, tmp_path):
     got = log.replay()
     assert 50 <= len(got) <= 60
     assert got == entries[:len(got)]
+
+
+@pytest.mark.gpu
+def test_small_flushes_route_to_the_cpu(tmp_path, oracle):
+    """VERDICT r4 Next 3: a flush whose frames total fewer than host_batch_max
+    bytes is checksummed on the flush thread's CPU (MI_CRC32C_CPU, counted in
+    host_flushes and the engine's host_batches), larger ones by the GPU
+    batch; the files are identical either way (replayed and CRC-checked by
+    the GPU scan).  The suite sets MI_DLOG_HOST_BATCH_MAX=0 (every flush on
+    the GPU); the environment override is lifted here, and a log made with
+    host_batch_max=0 never routes."""
+    import consus_amd as E
+    saved = os.environ.pop("MI_DLOG_HOST_BATCH_MAX")
+    try:
+        for hmax, routed in ((1 << 40, True), (0, False)):
+            log = DurableLog(1 << 20, host_batch_max=hmax)
+            d = tmp_path / f"d{hmax}"
+            assert log.open(str(d))
+            before = E.stats()["host_batches"]
+            entries = [os.urandom(20 + (i * 37) % 900) for i in range(3000)]
+            for i, e in enumerate(entries):
+                assert log.append(e) == i + 1
+            wait_durable(log, 3000)
+            hf, fl = log.host_flushes(), log.flushes()
+            assert fl > 0
+            if routed:
+                assert hf == fl and E.stats()["host_batches"] - before == fl
+            else:
+                assert hf == 0 and E.stats()["host_batches"] == before
+            log.close()
+            assert log.replay() == entries
+            n = 0
+            for f in ("file_a", "file_b"):
+                k, vb = scan_file(str(d / f))
+                assert vb == os.path.getsize(d / f)
+                n += k
+            assert n == 3000
+            for path in (d / "file_a", d / "file_b"):
+                for recno, entry, crc, hdr_entry in parse_frames(path):
+                    assert crc == oracle.crc32c(0, hdr_entry)
+            log.destroy()
+    finally:
+        os.environ["MI_DLOG_HOST_BATCH_MAX"] = saved
+
+
+def test_append_crc_hook_writes_the_reference_frames(tmp_path, reference, oracle):
+    """The reference scheme (bench hook, txman/durable_log.cc:215-218): every
+    appender computes its frame's CRC with the reference common/crc32c.cc on
+    its own thread; the flush thread checksums nothing.  The frames on disk
+    are the same as with a batch engine: every CRC checks."""
+    from consus_amd.durable_log import _lib
+    fn = C.cast(reference.lib.ref_crc32c, C.c_void_p).value
+    noop = C.cast(oracle.lib.oracle_dlog_batch, C.c_void_p).value
+    log = DurableLog(1 << 16, batch_crc=C.c_void_p(noop))
+    _lib().mi_dlog_set_append_crc_for_testing(log._h, C.c_void_p(fn))
+    d = tmp_path / "d"
+    assert log.open(str(d))
+    got, lock = {}, threading.Lock()
+
+    def worker(t):
+        for i in range(300):
+            e = bytes([t]) * (1 + (i * 53 + t) % 3000)
+            r = log.append(e)
+            assert r > 0
+            with lock:
+                got[r] = e
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wait_durable(log, 1200)
+    log.close()
+    frames = parse_frames(d / "file_a") + parse_frames(d / "file_b")
+    assert len(frames) == 1200
+    for recno, entry, crc, hdr_entry in frames:
+        assert got[recno] == entry and crc == oracle.crc32c(0, hdr_entry)
+    log.destroy()

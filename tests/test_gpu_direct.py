@@ -155,3 +155,42 @@ def test_zero_copy_needs_the_whole_span_mapped(engine, oracle):
     finally:
         assert hip.hipHostUnregister(addr) == 0
         del buf
+
+
+def test_zero_copy_two_registrations_with_a_pageable_gap(engine, oracle):
+    """ROCm reports hipHostRegister'ed memory with a null
+    allocation base, so the span check cannot bound a batch by one
+    allocation.  Two separately registered 1 MiB regions with a pageable
+    1 MiB gap between them, both ends of the batch mapped at device addresses
+    the right distance apart: the batch must be staged (its middle is not
+    mapped), bit-exact; batches inside either region stay zero-copy."""
+    import mmap
+
+    hip = _hip()
+    mib = 1 << 20
+    mm = mmap.mmap(-1, 3 * mib)
+    buf = np.frombuffer(mm, dtype=np.uint8)
+    buf[:] = np.random.default_rng(96).integers(0, 256, 3 * mib, dtype=np.uint8)
+    addr = buf.ctypes.data
+    assert hip.hipHostRegister(addr, mib, 0x3) == 0
+    try:
+        assert hip.hipHostRegister(addr + 2 * mib, mib, 0x3) == 0
+        try:
+            for lo in (0, 2 * mib):  # inside one registration: zero-copy
+                off = np.arange(32, dtype=np.uint64) * 8192 + np.uint64(lo + 77)
+                ln = np.full(32, 4000, dtype=np.uint32)
+                before = engine.stats()["zero_copy_batches"]
+                assert np.array_equal(engine.crc32c_batch(buf, off, ln), oracle.batch(buf, off, ln))
+                assert engine.stats()["zero_copy_batches"] - before == 1, lo
+            # first record in region 1, last in region 2, the gap between
+            # them untouched by any record but inside the batch's span
+            off = np.array([100, 2 * mib + 5000], dtype=np.uint64)
+            ln = np.array([6000, 9000], dtype=np.uint32)
+            before = engine.stats()["zero_copy_batches"]
+            assert np.array_equal(engine.crc32c_batch(buf, off, ln), oracle.batch(buf, off, ln))
+            assert engine.stats()["zero_copy_batches"] == before
+        finally:
+            assert hip.hipHostUnregister(addr + 2 * mib) == 0
+    finally:
+        assert hip.hipHostUnregister(addr) == 0
+        del buf

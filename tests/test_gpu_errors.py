@@ -156,3 +156,57 @@ def test_understated_size_hint_is_recovered(engine, oracle):
         assert np.array_equal(d_out.download(np.uint32, count), want)
     for b in (data, d_off, d_len, d_out):
         b.free()
+
+
+def test_understated_hint_on_an_async_batch_fails_the_next_sync(engine, oracle):
+    """an ASYNCHRONOUS sorted batch whose total_bytes hint
+    understates its records cannot be recomputed (nothing waits for it), and
+    its out[] is incomplete; the kernel sets a sticky word, and the calling
+    thread's next mi_crc32c_stream_sync reports it (EINVAL, counted in
+    hint_overflows) and clears it.  The sync after that, and a batch with a
+    true hint, are clean.  Runs in a fresh thread: a context whose
+    workspace the understated hint alone sizes."""
+    import threading
+    count = 64
+    lengths = np.full(count, 1 << 20, dtype=np.uint32)
+    offsets = (np.arange(count, dtype=np.uint64) << np.uint64(20)) + np.uint64(5)
+    size = (count << 20) + 4096
+    buf = np.random.default_rng(4).integers(0, 256, size, dtype=np.uint8)
+    data = engine.DeviceBuffer(size)
+    data.upload(buf)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    want = oracle.batch(buf, offsets, lengths)
+    seen = {}
+
+    def run():
+        try:
+            os.environ["MI_CRC32C_VARPATH"] = "sorted"
+            before = engine.stats()["hint_overflows"]
+            engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=4 << 20,
+                                asynchronous=True)
+            try:
+                engine.sync()
+                seen["first"] = "ok"
+            except engine.EngineError as e:
+                seen["first"] = e.status
+            seen["counted"] = engine.stats()["hint_overflows"] - before
+            engine.sync()  # cleared: clean
+            engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=int(lengths.sum()),
+                                asynchronous=True)
+            engine.sync()
+            seen["second"] = "ok"
+        except Exception as e:  # noqa: BLE001
+            seen["error"] = e
+        finally:
+            os.environ.pop("MI_CRC32C_VARPATH", None)
+    t = threading.Thread(target=run)
+    t.start()
+    t.join()
+    assert "error" not in seen, seen["error"]
+    assert seen["first"] == engine.EINVAL and seen["counted"] == 1 and seen["second"] == "ok", seen
+    assert np.array_equal(d_out.download(np.uint32, count), want)
+    for b in (data, d_off, d_len, d_out):
+        b.free()

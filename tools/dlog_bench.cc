@@ -12,12 +12,19 @@
 // files): every record must come back, in recno order, byte-exact.
 // Prints one JSON line.
 //
-// Engines of the flush thread's batch CRC: the GPU (default); with
-// REF_CRC_SO=path/to/oracle/_ref/libref_crc32c.so the reference
-// common/crc32c.cc itself (compiled unmodified, bench.py's CPU leg), called
-// per frame on the flush thread as the reference calls it per record
-// (txman/durable_log.cc:217-218) -- the same front-end with a CPU checksum,
-// timed in the same run.
+// Engines of the flush thread's batch CRC: the GPU (default; flushes below
+// the log's host_batch_max take the flush thread's CPU, MI_DLOG_HOST_BATCH_MAX
+// overrides); with REF_CRC_SO=path/to/oracle/_ref/libref_crc32c.so the
+// reference common/crc32c.cc itself (compiled unmodified, bench.py's CPU
+// leg), called per frame on the flush thread -- the same front-end with a
+// CPU checksum, timed in the same run.  With REF_SCHEME=1 as well, the
+// reference's own placement instead (txman/durable_log.cc:215-218): every
+// appender computes its frame's CRC with the reference function on its own
+// thread, outside any lock, and the flush thread checksums nothing.
+//
+// DLOG_ENTRY=zipf: entry lengths from the configs[2] distribution (Zipf,
+// 64 B - 64 KiB, mi_workload_zipf_lengths) instead of uniform in
+// [MIN_ENTRY, MAX_ENTRY].
 #include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -86,13 +93,16 @@ int main(int argc, char** argv)
     const std::string dir = argv[1];
     const int threads = atoi(argv[2]);
     const uint64_t per = strtoull(argv[3], nullptr, 10);
-    const uint32_t lo = uint32_t(atoi(argv[4])), hi = uint32_t(atoi(argv[5]));
+    uint32_t lo = uint32_t(atoi(argv[4])), hi = uint32_t(atoi(argv[5]));
     const size_t seg = argc > 6 ? size_t(strtoull(argv[6], nullptr, 10)) : 0;
     // a slower disk than tmpfs: every fsync also sleeps this long
     const uint32_t fsync_delay = argc > 7 ? uint32_t(strtoul(argv[7], nullptr, 10)) : 0;
     // diagnosis only: FAKE_CRC=1 replaces the GPU batch with a no-op (CRCs
     // left zero, replay not checked) to time the front-end alone
     const bool fake = getenv("FAKE_CRC") && atoi(getenv("FAKE_CRC"));
+    const bool ref_scheme = getenv("REF_SCHEME") && atoi(getenv("REF_SCHEME"));
+    const bool zipf = getenv("DLOG_ENTRY") && !strcmp(getenv("DLOG_ENTRY"), "zipf");
+    if (zipf) lo = 64, hi = 65536;
     if (threads < 1 || per < 1 || hi < lo)
     {
         fprintf(stderr, "bad arguments\n");
@@ -110,16 +120,21 @@ int main(int argc, char** argv)
     std::vector<std::vector<uint32_t>> lens(threads, std::vector<uint32_t>(per));
     std::vector<std::vector<uint64_t>> offs(threads, std::vector<uint64_t>(per));
     uint64_t entry_bytes = 0;
+    // configs[2]'s lengths: thread t takes records t*per .. of the stream
+    if (zipf)
+        for (int t = 0; t < threads; ++t)
+            mi_workload_zipf_lengths(0x5EED, uint64_t(t) * per, per, lens[t].data());
     for (int t = 0; t < threads; ++t)
         for (uint64_t k = 0; k < per; ++k)
         {
             const uint64_t r = splitmix64((uint64_t(t) << 40) ^ k ^ 0x5EEDull);
-            lens[t][k] = lo + uint32_t(r % (hi - lo + 1));
+            if (!zipf) lens[t][k] = lo + uint32_t(r % (hi - lo + 1));
             offs[t][k] = (r >> 20) % (pool_bytes - hi);
             entry_bytes += lens[t][k];
         }
 
     std::vector<std::pair<size_t, double>> g_link;  // (bytes, us) of pinned-to-device copies
+    std::vector<std::pair<size_t, double>> g_cpu;   // (bytes, us) of the CPU path's batch
     const char* ref_so = getenv("REF_CRC_SO");
     if (ref_so && *ref_so)
     {
@@ -177,6 +192,35 @@ int main(int argc, char** argv)
                 g_link.push_back({n, t[t.size() / 2]});
             }
         }
+        // the flush thread's CPU path as a routed flush sees it: frames of
+        // the run's entry sizes checksummed by mi_crc32c_batch(MI_CRC32C_CPU)
+        if (hp)
+        {
+            const unsigned char* b = static_cast<const unsigned char*>(hp);
+            for (size_t n : {size_t(64) << 10, size_t(256) << 10, size_t(1) << 20, size_t(4) << 20})
+            {
+                std::vector<uint64_t> o;
+                std::vector<uint32_t> l;
+                for (uint64_t at = 0, k = 0; at < n; ++k)
+                {
+                    const uint32_t e = std::min<uint64_t>(
+                        16 + (zipf ? 4700 : (lo + hi) / 2) + 4, n - at);
+                    o.push_back(at);
+                    l.push_back(e > 4 ? e - 4 : e);
+                    at += e;
+                }
+                std::vector<uint32_t> c(o.size());
+                std::vector<double> t;
+                for (int i = 0; i < 25; ++i)
+                {
+                    const double a = now();
+                    mi_crc32c_batch(b, o.data(), l.data(), nullptr, o.size(), 0, c.data(), MI_CRC32C_CPU);
+                    if (i >= 5) t.push_back((now() - a) * 1e6);
+                }
+                std::sort(t.begin(), t.end());
+                g_cpu.push_back({n, t[t.size() / 2]});
+            }
+        }
         if (dp) mi_dev_free(dp);
         if (hp) mi_host_free_pinned(hp);
     }
@@ -218,7 +262,14 @@ int main(int argc, char** argv)
             }
         }
     });
-    if (g_ref) log.set_batch_crc_for_testing(ref_batch, nullptr);
+    if (g_ref && ref_scheme)
+    {
+        // the reference scheme: the appenders checksum, the flush thread
+        // does not (the batch engine stays the default: the replay's scan)
+        log.set_append_crc_for_testing(g_ref);
+    }
+    else if (g_ref)
+        log.set_batch_crc_for_testing(ref_batch, nullptr);
     if (fake)
         log.set_batch_crc_for_testing(
             [](void*, const void*, const uint64_t*, const uint32_t*, size_t n, uint64_t,
@@ -317,6 +368,7 @@ int main(int argc, char** argv)
     std::sort(lat.begin(), lat.end());
     auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[size_t(q * (lat.size() - 1))]; };
     const uint64_t flushes = log.flushes(), frames = log.frames_flushed();
+    const uint64_t host_flushes = log.host_flushes();
     const int err = log.error();
     double fs[6], fm[6];
     log.flush_seconds(fs);
@@ -347,7 +399,15 @@ int main(int argc, char** argv)
         link += b;
     }
     link += "}";
-    printf("{\"engine\": \"%s\", \"link_us\": %s, \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
+    std::string cpu = "{";
+    for (size_t i = 0; i < g_cpu.size(); ++i)
+    {
+        char b[64];
+        snprintf(b, sizeof b, "%s\"%zu\": %.2f", i ? ", " : "", g_cpu[i].first, g_cpu[i].second);
+        cpu += b;
+    }
+    cpu += "}";
+    printf("{\"engine\": \"%s\", \"entries\": \"%s\", \"host_flushes\": %llu, \"cpu_batch_us\": %s, \"link_us\": %s, \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
            "\"append_s\": %.6f, \"durable_s\": %.6f, \"appends_per_s\": %.1f, "
            "\"frame_GiB_per_s\": %.4f, \"flushes\": %llu, \"frames_flushed\": %llu, "
            "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
@@ -357,7 +417,9 @@ int main(int argc, char** argv)
            "\"patch\": %.1f, \"pwrite\": %.1f, \"fsync\": %.1f}, "
            "\"durable_latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, "
            "\"max_at_s\": %.4f, \"samples\": %zu}}\n",
-           fake ? "none" : g_ref ? "reference-cpu" : "gpu", link.c_str(), empty_us, threads,
+           fake ? "none" : g_ref ? (ref_scheme ? "reference-scheme" : "reference-cpu") : "gpu",
+           zipf ? "zipf 64 B - 64 KiB" : "uniform", (unsigned long long)host_flushes, cpu.c_str(), link.c_str(),
+           empty_us, threads,
            (unsigned long long)total,
            (unsigned long long)entry_bytes,
            (unsigned long long)frame_bytes, t_appended - t0, t_durable - t0,

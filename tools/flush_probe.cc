@@ -10,7 +10,9 @@
 // by copy commands (MI_CRC32C_ZERO_COPY=0), of the direct kernel with its LDS
 // table image (MI_CRC32C_DIRECT_LITE=0), of the default form waited for by a
 // stream sync (MI_CRC32C_DONE_WORD=0), of a one-record round trip (16 B),
-// and the bound 'round trip + bytes / 55 GB/s'.
+// the bound 'round trip + bytes / 55 GB/s', and the engine's CPU path on the
+// calling thread (MI_CRC32C_CPU: crc32q, what the durable log routes flushes
+// below its host_batch_max to; round 5).
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -60,9 +62,9 @@ int main(int argc, char** argv)
         x ^= x << 13, x ^= x >> 7, x ^= x << 17;
         arena[i] = (unsigned char)x;
     }
-    printf("%7s %9s %10s %10s %10s %10s %10s %10s %10s\n", "frames", "bytes", "multi_us",
-           "batch_us", "copy_us", "lds_us", "sync_us", "empty_us", "bound_us");
-    for (size_t frames : {1, 16, 64, 128, 270, 512, 1024, 2048, 4096, 8192})
+    printf("%7s %9s %10s %10s %10s %10s %10s %10s %10s %10s\n", "frames", "bytes", "multi_us",
+           "batch_us", "copy_us", "lds_us", "sync_us", "empty_us", "bound_us", "cpu_us");
+    for (size_t frames : {1, 16, 64, 128, 270, 384, 512, 640, 768, 1024, 2048, 4096, 8192})
     {
         std::vector<uint64_t> off(frames);
         std::vector<uint32_t> len(frames);
@@ -113,9 +115,14 @@ int main(int argc, char** argv)
         const double empty = median_us(reps, [&] {
             mi_crc32c_batch(arena, &o16, &l16, nullptr, 1, 16, &c16, MI_CRC32C_FALLBACK);
         });
-        printf("%7zu %9llu %10.2f %10.2f %10.2f %10.2f %10.2f %10.2f %10.2f\n", frames,
+        const double cpu = median_us(reps, [&] {
+            mi_crc32c_batch(arena, off.data(), len.data(), nullptr, frames, total, out2.data(),
+                            MI_CRC32C_CPU);
+        });
+        if (memcmp(out.data(), out2.data(), frames * 4)) printf("MISMATCH cpu\n");
+        printf("%7zu %9llu %10.2f %10.2f %10.2f %10.2f %10.2f %10.2f %10.2f %10.2f\n", frames,
                (unsigned long long)at, multi, batch, copy, lds, sync, empty,
-               empty + double(at) / 55e3);
+               empty + double(at) / 55e3, cpu);
         fflush(stdout);
     }
     mi_crc32c_stats_t st;

@@ -5,7 +5,7 @@
 #   tools/session.sh tests route crossover rehearsal dlog zipf fixed ...
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$ROOT/gpurun_out/${SESSION:-r04}"
+OUT="$ROOT/gpurun_out/${SESSION:-r05}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT" || exit 9
@@ -99,6 +99,13 @@ while [ $# -gt 0 ]; do
              done | tee "$OUT/fetchab.out" ;;
     fusedab) for fz in 1 0; do MI_CRC32C_SORT_FUSED=$fz run mid_fused$fz 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,4,16,64,256} --reps 100 || exit 1; done ;;
     zipfring) for rnd in 1 2 3; do for rg in 2 4; do echo -n "round $rnd ring $rg "; MI_CRC32C_SORT_RING=$rg timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"; done; done | tee "$OUT/zipfring.out" ;;
+    # round 5: the records' shared 128-B lines (ZIPF_ALIGN=128 starts every
+    # record on its own line; wrong digest by design), per library in tools/ab
+    align) for rnd in 1 2; do for al in 0 128; do for lib in ${ALIGN_LIBS:-r04}; do
+               echo -n "round $rnd align=$al $lib "; ZIPF_ALIGN=$al timeout -k 10 120 python3 tools/zipf_probe.py tools/ab/libconsus_crc32c_$lib.so > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done; done; done | tee "$OUT/align.out" ;;
+    gpusorted) run pytest_sorted 900 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_parity.py tests/test_gpu_errors.py tests/test_gpu_direct.py -x -q --timeout 120 --timeout-method thread ;;
+    stamps) for m in ${STAMP_MIB:-0 256 1}; do echo "== mib $m"; timeout -k 10 120 python3 tools/sort_stamps.py tools/ab/libconsus_crc32c_${STAMP_LIB:-stamp}.so --mib $m || exit 1; done | tee "$OUT/stamps.out" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

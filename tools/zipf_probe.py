@@ -26,6 +26,14 @@ if os.environ.get("ZIPF_DROP_BELOW"):
     ln = np.where(ln < int(os.environ["ZIPF_DROP_BELOW"]), 0, ln).astype(ln.dtype)
 if os.environ.get("ZIPF_KEEP_BELOW"):
     ln = np.where(ln < int(os.environ["ZIPF_KEEP_BELOW"]), ln, 0).astype(ln.dtype)
+# ZIPF_ALIGN=n: every record starts on an n-byte boundary (gaps between them;
+# no 128-B line shared by two records at n = 128; wrong digest by design)
+if int(os.environ.get("ZIPF_ALIGN", "0") or 0) > 0:
+    al = int(os.environ["ZIPF_ALIGN"])
+    padded = ((ln.astype(np.uint64) + np.uint64(al - 1)) // np.uint64(al)) * np.uint64(al)
+    off = np.zeros(R, dtype=np.uint64)
+    off[1:] = np.cumsum(padded[:-1], dtype=np.uint64)
+    total = int(off[-1] + padded[-1])
 data = E.DeviceBuffer(total + 16)
 data.fill_splitmix64(W.DATA_SEED)
 d_off, d_len, out = E.DeviceBuffer(R * 8), E.DeviceBuffer(R * 4), E.DeviceBuffer(R * 4)
