@@ -576,8 +576,11 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
             for _ in range(PMC_CHILD_STEPS):
                 E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
             return {}
+        # one synchronous step (it checks the size hint's overflow flag), then
+        # the warm-up back to back, as the timed steps run
+        E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
         for _ in range(args.warmup):
-            E.device_batch(data, d_off, d_len, R, out, total_bytes=total)
+            E.device_batch(data, d_off, d_len, R, out, total_bytes=total, asynchronous=True)
         E.sync()
         sorted0 = E.stats().get("sorted_batches", 0)
         t0 = time.perf_counter()

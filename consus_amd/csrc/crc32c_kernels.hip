@@ -2038,10 +2038,14 @@ struct SortShared
     uint32_t n_full;           // full pieces (listed first: the largest items)
     uint32_t full_base;        // their slots: items[count + full_base ...]
     uint32_t next_group;
-    uint32_t next_lane;        // lane items taken (64 per grab)
+    uint32_t next_lane;        // lane items taken (64 per grab; without help)
+    uint32_t teams_done;       // waves past their team groups (the first publishes)
+    uint32_t help_arrived;     // waves at the help phase (the first polls the ring)
+    uint32_t help_word;        // the poller's announcement: gen << 12 | victim; ~0: done
     uint32_t lane_base;        // the first lane item's position among the last pieces
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
+    uint32_t bar_ok;           // fused launch: the grid barrier completed
     uint64_t pre[2];           // cost before those blocks
     uint64_t target[2];
     uint64_t total;            // the batch's total cost C
@@ -2100,7 +2104,9 @@ __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ bl
         for (uint32_t k = 0; k < K; ++k)
         {
             const uint32_t j = c0 + lane * K + k;
-            v[k] = j < nb ? blk_cost[j] : 0;
+            // sc1 loads: in a fused launch other workgroups stored these
+            // costs (sc1, write-through) before the grid barrier
+            v[k] = j < nb ? __hip_atomic_load(blk_cost + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
         }
 #pragma unroll
         for (uint32_t k = 0; k < K; ++k) tot += v[k];
@@ -2140,7 +2146,8 @@ __device__ __forceinline__ void sort_find_blocks(const uint64_t* __restrict__ bl
         for (uint32_t k = 0; k < K; ++k)
         {
             const uint32_t j = c0 + lane * K + k;
-            if (!one_round) v[k] = j < nb ? blk_cost[j] : 0;
+            if (!one_round)
+                v[k] = j < nb ? __hip_atomic_load(blk_cost + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
             sum += v[k];
         }
         const uint64_t incl = carry + wave_incl_scan64(sum), excl = incl - sum;
@@ -2319,6 +2326,114 @@ __device__ __forceinline__ uint32_t zshift48(const uint32_t* __restrict__ pow2, 
     return v;
 }
 
+// One-launch form (round 5, VERDICT r4 Next 1a): the work of
+// sorted_cost_kernel done by the hash kernel's own workgroups, then a grid
+// barrier, so the batch needs no second launch.  Workgroup b computes cost
+// blocks b, b + G, ... (up to four per round, every load issued first),
+// stores each block's sum and every split record's ~0 (the identity its
+// pieces XOR into) with write-through (sc1) stores, drains them (vmcnt(0),
+// every wave), and arrives at the barrier: one agent-scope add per workgroup
+// on a monotonic counter (ctrl[32]; this launch's arrivals take it from
+// bar_base to bar_base + G), polled with sc1 loads (MI355X_MICROARCH.md,
+// inter-workgroup visibility, the table's first row: sc1 stores, one atomic
+// add per workgroup, sc1 loads of the handed-off words -- sort_find_blocks
+// reads the block costs with sc1 loads; the pieces' XORs are memory-side
+// atomics, after the barrier).  The engine launches this form only when the
+// grid fits one workgroup per CU and no other thread's context of the
+// process uses the sorted path on the device (two barrier launches sharing
+// the CUs could wait on each other); even so the wait is bounded: after
+// kSortBarrierTicks the workgroup stores ctrl[3] = bar_base + G + 1 (and the
+// sticky ctrl[2]) and returns, and the host recomputes the batch with the two
+// launches (a synchronous batch) or reports it at the next stream sync.
+constexpr uint64_t kSortBarrierTicks = 5000000;  // 50 ms at s_memrealtime's 100 MHz
+template <typename SS>
+__device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const uint64_t* off,
+                                                   const uint32_t* len, const uint32_t* inits,
+                                                   uint64_t count, uint64_t* blk_cost, uint32_t nb,
+                                                   uint32_t* ctrl, uint32_t* out,
+                                                   const uint32_t* tables, uint32_t plog,
+                                                   uint32_t bar_base, SS& S)
+{
+    constexpr uint32_t CX = 4;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t G = gridDim.x;
+    // per-wave sums in the table image's LDS (free until the binning)
+    uint64_t* const wsum = reinterpret_cast<uint64_t*>(smem);
+    for (uint64_t j0 = blockIdx.x; j0 < nb; j0 += CX * G)
+    {
+        uint64_t av[CX];
+        uint32_t Lv[CX];
+#pragma unroll
+        for (uint32_t x = 0; x < CX; ++x)
+        {
+            const uint64_t r = (j0 + x * G) * kSortRecs + threadIdx.x;
+            const bool in = j0 + x * G < nb && r < count;
+            av[x] = in ? off[r] : 0;
+            Lv[x] = in ? len[r] : 0;
+        }
+#pragma unroll
+        for (uint32_t x = 0; x < CX; ++x)
+        {
+            const uint64_t r = (j0 + x * G) * kSortRecs + threadIdx.x;
+            const bool in = j0 + x * G < nb && r < count;
+            uint64_t c = 0;
+            if (in)
+            {
+                const uint8_t* p = base + av[x];
+                const uint32_t L = Lv[x];
+                if (L < 4)
+                {
+                    uint32_t h = ~(inits ? inits[r] : 0u);
+                    for (uint32_t i = 0; i < L; ++i) h = tables[kTabT + ((h ^ p[i]) & 0xFFu)] ^ (h >> 8);
+                    out[r] = ~h;
+                }
+                else
+                {
+                    const SortCost sc = sort_cost(uint64_t(p), L, plog);
+                    c = sc.cost;
+                    if (sc.n > 1) __hip_atomic_store(out + r, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+            if (lane == 0) wsum[x * 16 + wave] = c;
+        }
+        __syncthreads();
+        if (threadIdx.x < CX && j0 + threadIdx.x * G < nb)
+        {
+            uint64_t t = 0;
+            for (uint32_t w = 0; w < kBlock / 64; ++w) t += wsum[threadIdx.x * 16 + w];
+            __hip_atomic_store(blk_cost + j0 + threadIdx.x * G, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // overflow flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores written through
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        __hip_atomic_fetch_add(ctrl + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = true;
+        while (uint32_t(__hip_atomic_load(ctrl + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - bar_base) <
+               uint32_t(G))
+        {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kSortBarrierTicks)
+            {
+                ok = false;
+                __hip_atomic_store(ctrl + 3, bar_base + uint32_t(G) + 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        S.bar_ok = ok;
+    }
+    __syncthreads();
+    return S.bar_ok != 0;
+}
+
 // Phase stamps of the sorted kernel (dev builds only: tools/build_variant.sh
 // TAG -DMI_SORT_STAMP=1, read by tools/sort_stamps.py through
 // mi_debug_sort_stamps): lane 0 of every wave of workgroups < 256 stores
@@ -2327,6 +2442,9 @@ __device__ __forceinline__ uint32_t zshift48(const uint32_t* __restrict__ pow2, 
 // groups done, lane items done, finish done.  Off in the product build.
 #ifndef MI_SORT_STAMP
 #define MI_SORT_STAMP 0
+#endif
+#ifndef MI_SORT_LANE_BLOCKS
+#define MI_SORT_LANE_BLOCKS 16
 #endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
@@ -2348,10 +2466,11 @@ template <int RB>
 __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
-    const uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
+    uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
-    uint32_t lrows)
+    uint32_t lrows, int fused, uint32_t bar_base, uint64_t* __restrict__ help, uint32_t help_epoch,
+    uint32_t ring_base)
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint64_t piece = uint64_t(1) << plog;
@@ -2361,6 +2480,29 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     if (threadIdx.x == 0) S.next_lane = 0;
+    if (threadIdx.x == 0) S.teams_done = S.help_arrived = S.help_word = 0;
+    // Help with lane items across workgroups (DESIGN.md section 4.7, round
+    // 5): the help workspace H holds the ring counter (word 0), the ring of
+    // published workgroups (words 16 ..), and per workgroup v its record at
+    // word 16 + kSortHelpMaxGrid + 8 v: two granules {tag, lane items} and
+    // {tag, list start}, then its lane cursor.
+    const bool helping = help && gridDim.x > 1 && gridDim.x <= kSortHelpMaxGrid;
+    auto pubA = [&](uint32_t v) { return help + 16 + kSortHelpMaxGrid + 8 * uint64_t(v); };
+    auto curp = [&](uint32_t v) { return reinterpret_cast<uint32_t*>(pubA(v) + 2); };
+    // every workgroup appends itself to the ring exactly once per launch (the
+    // host advances ring_base by the grid), with its lane list or none
+    auto publish = [&](uint32_t n_lane, uint32_t list_start) {
+        __hip_atomic_store(pubA(blockIdx.x), (uint64_t(help_epoch) << 32) | n_lane, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pubA(blockIdx.x) + 1, (uint64_t(help_epoch) << 32) | list_start,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the granules before the ring entry
+        const uint32_t k = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(help), 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) - ring_base;
+        if (k < kSortHelpMaxGrid)
+            __hip_atomic_store(help + 16 + k, (uint64_t(help_epoch) << 32) | blockIdx.x, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
     // whole records finished in the loop (RB = 4, small batches) or by the
@@ -2371,6 +2513,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // (1) Wave 0: the two targets and the cost blocks holding them, while the
     // other waves stage the tables (the staging's barrier covers both).
     SORT_STAMP(0);
+    if (fused && !sorted_fused_costs(base, off, len, inits, count, blk_cost, nb, ctrl, out, tables,
+                                     plog, bar_base, S))
+    {
+        if (helping && threadIdx.x == 0) publish(0, 0);
+        return;  // the grid barrier timed out: ctrl[3] tells the host (below)
+    }
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
     SORT_STAMP(1);
@@ -2442,6 +2590,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto put = [&](uint4* dst, const uint4& dv) {
         __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
     };
+    // Lane-item descriptors, when other workgroups may help with them:
+    // write-through (sc1) stores, which other CUs read with sc1 loads without
+    // a release/acquire pair (MI355X_MICROARCH.md, inter-workgroup visibility)
+    auto put_shared = [&](uint4* dst, const uint4& dv) {
+        uint64_t* const q = reinterpret_cast<uint64_t*>(dst);
+        __hip_atomic_store(q, uint64_t(dv.x) | (uint64_t(dv.y) << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, uint64_t(dv.z) | (uint64_t(dv.w) << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    };
     // Up to kLdsBytes / 16 items, the descriptors go to LDS at their list
     // position (the table image's space: the tables are staged after), and
     // then out in list order, whole lines: scattered 16-B stores cost the
@@ -2455,6 +2613,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     auto put_last = [&](uint32_t pos, const uint4& dv) {
         if (staged) stage_lds[stage_nf + pos] = dv;
+        else if (helping && pos >= S.lane_base) put_shared(lastv + pos, dv);
         else put(lastv + pos, dv);
     };
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
@@ -2561,13 +2720,30 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         else
             pass(true);
     }
+    if (helping) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (helpers read lane descriptors)
     __syncthreads();
-    if (n_items == 0) return;
+    if (n_items == 0)
+    {
+        if (helping && threadIdx.x == 0) publish(0, 0);
+        return;
+    }
+    if (helping && threadIdx.x == 0)
+    {
+        __hip_atomic_store(curp(blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (staged)
     {
         // list order out: full pieces to their region, the rest after rlo
         for (uint32_t i = threadIdx.x; i < n_items; i += kBlock)
-            put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
+        {
+            uint4* const dst = i < n_full ? fullv + S.full_base + i : lastv + (i - n_full);
+            if (helping && i >= n_full + S.lane_base)
+                put_shared(dst, stage_lds[i]);  // a lane item: helpers read it
+            else
+                put(dst, stage_lds[i]);
+        }
+        if (helping) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     stage_tables(tables);  // ends with a barrier
@@ -2668,16 +2844,26 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // finish.  The list is ordered by block count, so the lanes of a wave run
     // about the same number of steps.  Blocks are read with the default
     // policy: a block's line is shared with the neighbouring records.
-    auto lane_items = [&]() {
-        const uint32_t n_lane = n_items - n_long;
-        const uint4* const listLane = listL + n_long;
+    // One list of lane items: this workgroup's (cur: its global cursor when
+    // helping, else null: the LDS counter) or a victim's (its cursor).
+    // blocks of one lane item loaded at once (a multiple of 4; the rest of a
+    // longer item takes another round)
+    constexpr int32_t kLaneBlocks = MI_SORT_LANE_BLOCKS;
+    auto lane_items = [&](const uint4* listLane, uint32_t n_lane, uint32_t* cur) __attribute__((always_inline)) {
         auto grab64 = [&]() {
             uint32_t c = 0;
-            if (lane == 0) c = atomicAdd(&S.next_lane, 64u);
+            if (lane == 0)
+                c = cur ? __hip_atomic_fetch_add(cur, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : atomicAdd(&S.next_lane, 64u);
             return uint32_t(__builtin_amdgcn_readfirstlane(int(c)));
         };
         auto ldesc = [&](uint32_t c) {
-            return c + lane < n_lane ? listLane[c + lane] : make_uint4(0, 0, 0, 0);
+            if (c + lane >= n_lane) return make_uint4(0, 0, 0, 0);
+            if (!cur) return listLane[c + lane];
+            const uint64_t* q = reinterpret_cast<const uint64_t*>(listLane + c + lane);
+            const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
         };
         // Latency (round 5): a grab used to be three dependent global round
         // trips or more (its descriptors, then its blocks four at a time,
@@ -2713,18 +2899,18 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             const uint4 kf = make_uint4(keep_from(int32_t(q), 0), keep_from(int32_t(q), 1),
                                         keep_from(int32_t(q), 2), keep_from(int32_t(q), 3));
             uint32_t st = 0;
-            for (int32_t j = 0; __builtin_amdgcn_ballot_w64(j < nb) != 0; j += 16)
+            for (int32_t j = 0; __builtin_amdgcn_ballot_w64(j < nb) != 0; j += kLaneBlocks)
             {
-                uint4 w[16];
+                uint4 w[kLaneBlocks];
 #pragma unroll
-                for (int u = 0; u < 16; ++u)
+                for (int u = 0; u < int(kLaneBlocks); ++u)
                 {
                     w[u] = make_uint4(0, 0, 0, 0);
                     if (__builtin_amdgcn_ballot_w64(j + u < nb) != 0)  // wave-uniform
                         w[u] = load16_edge(j + u < nb ? pb + 16 * (j + u) : zero16);
                 }
 #pragma unroll
-                for (int u4 = 0; u4 < 16; u4 += 4)
+                for (int u4 = 0; u4 < int(kLaneBlocks); u4 += 4)
                 {
                     if (__builtin_amdgcn_ballot_w64(j + u4 < nb) == 0) break;
 #pragma unroll
@@ -2941,9 +3127,22 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     flush();
 
     SORT_STAMP(5);
-    lane_items();
+    const uint32_t n_lane_own = n_items - n_long;
+    if (helping)
+    {
+        // the first wave past its team groups publishes the lane list: its
+        // descriptors went out write-through (sc1) and every wave drained
+        // them (vmcnt(0)) before the prologue's barriers; the granules and
+        // the ring entry follow (helpers read everything with sc1 loads)
+        uint32_t ord = 0;
+        if (lane == 0) ord = atomicAdd(&S.teams_done, 1u);
+        ord = uint32_t(__builtin_amdgcn_readfirstlane(int(ord)));
+        if (ord == 0 && lane == 0) publish(n_lane_own, uint32_t(rlo - n_full + n_long));
+    }
+    lane_items(listL + n_long, n_lane_own, helping ? curp(blockIdx.x) : nullptr);
     SORT_STAMP(6);
-    if (INLOOP) return;  // whole records were finished in the loop
+    if (!INLOOP)
+    {
     // Finish pass, in list order (round 5): a whole record's fold value W
     // (wr at its slot, eight consecutive words per group) is Z_m(raw) of its
     // bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).  The team items past the
@@ -2986,7 +3185,88 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             if (!(dv[u].w & kSortMulti)) out[dv[u].w & kSortRecMask] = ~v;
         }
     }
+    }  // !INLOOP
     SORT_STAMP(7);
+    if (!helping) return;
+    // Help phase: this workgroup is done; its waves take lane items of the
+    // workgroups still running (the slowest publish last).  The first wave
+    // here polls the ring; when an entry names a workgroup with lane items
+    // left, it announces it in LDS and every wave here drains that list
+    // through its cursor (claims are atomic: each item is hashed once, by its
+    // owner or a helper).  Bounded: the poller stops once every workgroup has
+    // published and been examined, or after kSortHelpTicks.
+    constexpr uint64_t kSortHelpTicks = 3000;  // 30 us
+    auto steal = [&](uint32_t v) {
+        const uint64_t ga = __hip_atomic_load(pubA(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t gb = __hip_atomic_load(pubA(v) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((ga >> 32) != help_epoch || (gb >> 32) != help_epoch) return;
+        lane_items(items + uint32_t(gb), uint32_t(ga), curp(v));
+    };
+    uint32_t ord = 0;
+    if (lane == 0) ord = atomicAdd(&S.help_arrived, 1u);
+    ord = uint32_t(__builtin_amdgcn_readfirstlane(int(ord)));
+    const uint32_t G = gridDim.x;
+    if (ord == 0)
+    {
+        uint32_t pos = 0, gen = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;)
+        {
+            const uint32_t avail = min(__hip_atomic_load(reinterpret_cast<uint32_t*>(help), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) - ring_base, G);
+            if (pos < avail)
+            {
+                const uint32_t i = pos + lane;
+                const bool in = i < avail;
+                const uint64_t e = in ? __hip_atomic_load(help + 16 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0;
+                const bool valid = in && (e >> 32) == help_epoch;
+                // the valid prefix (an entry is stored just after its slot is taken)
+                const uint64_t bad = __builtin_amdgcn_ballot_w64(in && !valid);
+                const uint32_t nvalid = bad ? uint32_t(__builtin_ctzll(bad)) : min(avail - pos, 64u);
+                const uint32_t v = uint32_t(e);
+                const bool look = valid && lane < nvalid && v != blockIdx.x;
+                const uint64_t ga = look ? __hip_atomic_load(pubA(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                const uint32_t cu = look ? __hip_atomic_load(curp(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                uint64_t wm = __builtin_amdgcn_ballot_w64(look && (ga >> 32) == help_epoch && cu < uint32_t(ga));
+                while (wm)
+                {
+                    const int k = __builtin_ctzll(wm);
+                    wm &= wm - 1;
+                    const uint32_t vk = uint32_t(__builtin_amdgcn_readlane(int(v), k));
+                    ++gen;
+                    if (lane == 0)
+                        __hip_atomic_store(&S.help_word, (gen << 12) | vk, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    steal(vk);
+                }
+                pos += nvalid;
+                if (nvalid == 0) __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            if (avail >= G) break;  // every workgroup published and was examined
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kSortHelpTicks) break;
+            __builtin_amdgcn_s_sleep(16);
+        }
+        if (lane == 0)
+            __hip_atomic_store(&S.help_word, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    else
+    {
+        uint32_t seen = 0;
+        for (;;)
+        {
+            const uint32_t w = __hip_atomic_load(&S.help_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (w == 0xFFFFFFFFu) break;
+            if ((w >> 12) != seen)
+            {
+                seen = w >> 12;
+                steal(w & 0xFFFu);
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
 }
 
 #if MI_SORT_STAMP
@@ -3016,12 +3296,14 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     if (count == 0) return hipSuccess;
     const uint32_t nb = sorted_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
-    hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
-                       lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
+    if (!ws.fused)
+        hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
+                           lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
     auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog, ws.lane_rows);
+                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base, ws.help, ws.help_epoch,
+                       ws.ring_base);
     return hipGetLastError();
 }
 

@@ -89,10 +89,13 @@ constexpr uint64_t kBatchFrameMax = uint64_t(1) << 30;
 
 // Flushes below this many frame bytes are checksummed on the flush thread's
 // CPU (the engine's crc32q loop, MI_CRC32C_CPU): the GPU batch's floor (a
-// launch, zero-copy reads over PCIe and the completion word, ~11-12 us) costs
-// more there than the CPU loop's ~13 GB/s.  The crossover measured per flush
-// size with tools/flush_probe.
-constexpr uint64_t kHostBatchMaxDefault = uint64_t(384) << 10;
+// launch, zero-copy reads over PCIe and the completion word, ~11.5 us) costs
+// more there than the CPU loop (~19 GB/s on the GPU box's EPYC 9575F).
+// Measured per flush size with tools/flush_probe, medians of 1,000
+// (profiles/r05_flush_probe.txt): 215 KB 19.6 us GPU / 10.9 CPU, 429 KB
+// 25.6 / 21.9, 569 KB 29.9 / 29.2, 1.12 MB 44.3 / 58.6; they cross near
+// 550 KB.
+constexpr uint64_t kHostBatchMaxDefault = uint64_t(512) << 10;
 
 uint64_t host_batch_max(const consus::durable_log_options& o)
 {

@@ -77,6 +77,9 @@ struct DeviceState
     Op32 pow2_ops[64];             // host copies for mi_crc32c_combine
     uint32_t crc0 = 0;             // crc32c(0, 4096 zero bytes): chunk CRC -> raw register
     std::string arch;
+    // thread contexts of this process that have run the sorted path on the
+    // device: the one-launch (grid-barrier) form only while it is 1
+    std::atomic<int> sorted_users{0};
 };
 
 std::mutex g_mu;
@@ -328,6 +331,7 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
+    DevBuf srt_help;                       // its cross-workgroup lane help (zeroed once)
     DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
     uint32_t done_seq = 0;
     PinBuf pin_small;                   // plan-size read-back; word kDoneWord: completion word
@@ -340,6 +344,14 @@ struct Ctx
     // an asynchronous sorted batch ran since the last stream sync: its
     // overflow (understated size hint) sits in the sticky ctrl[2]
     bool async_sorted_unchecked = false;
+    // the one-launch sorted form: this context counted in its device's
+    // sorted_users, and the barrier counter's value before the next launch
+    std::atomic<int>* sorted_users = nullptr;
+    uint32_t bar_base = 0;
+    bool force_unfused = false;  // the retry after a timed-out barrier
+    uint32_t help_epoch = 0;     // the last help tag used (never 0)
+    uint32_t ring_base = 0;      // the help ring counter before the next launch
+    uint32_t bar_tag = 0;        // ctrl[3] if the last one-launch batch's barrier timed out
     uint32_t* plan_total = nullptr;
     uint64_t plan_cap = 0;
 
@@ -409,9 +421,11 @@ struct Ctx
     void release()
     {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (sorted_users) sorted_users->fetch_sub(1);
+        sorted_users = nullptr;
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs, &srt_cost,
-                          &srt_ctrl, &srt_items, &done_ctr})
+                          &srt_ctrl, &srt_items, &srt_help, &done_ctr})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -629,6 +643,35 @@ uint32_t sorted_lane_rows()
     return kSortLaneRows;
 }
 
+// The one-launch sorted form (a grid barrier, crc32c_kernels.hip
+// sorted_fused_costs) needs every workgroup resident: one per CU, so at most
+// `cus` of them, and no second barrier launch sharing the CUs -- so only
+// while this is the process's one context that runs the sorted path on the
+// device.  Measured slower than the two launches (round 5, interleaved on one
+// box: configs[2] 0.7708-0.7732 ms against 0.7678-0.7690; 16 / 64 / 256 MiB
+// 26.7 / 34.1 / 67.7 us against 24.9 / 31.5 / 63.6; profiles/r05_fused_ab.txt):
+// the barrier's fan-in of 256 agent-scope adds on one word plus the
+// write-through drain cost more than the cost kernel's launch.  Off unless
+// MI_CRC32C_SORT_FUSED=1 (A/B, tests; read per batch).
+bool fused_ok(DeviceState* d, const Ctx* c, int grid)
+{
+    if (c->force_unfused) return false;
+    const char* e = std::getenv("MI_CRC32C_SORT_FUSED");
+    if (!e || std::strcmp(e, "1")) return false;
+    return grid <= d->cus && d->sorted_users.load() == 1;
+}
+
+// Cross-workgroup help with lane items (crc32c_kernels.hip, the help phase),
+// for batches of at least kSortHelpMinCount records: MI_CRC32C_SORT_HELP=0
+// turns it off, =2 on at every size (A/B, tests; read per batch).
+bool sorted_help_on(uint64_t count)
+{
+    const char* e = std::getenv("MI_CRC32C_SORT_HELP");
+    if (e && !std::strcmp(e, "0")) return false;
+    if (e && !std::strcmp(e, "2")) return true;
+    return count >= kSortHelpMinCount;
+}
+
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
 int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
@@ -643,20 +686,42 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
         grid = std::max(1, std::min(8 * grid, std::atoi(e)));
     const uint64_t cap = sorted_item_cap(count, total_bytes, plog, grid);
     int st;
+    const bool help = sorted_help_on(count) && grid > 1 && grid <= int(kSortHelpMaxGrid);
     if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
         (st = reserve_zeroed(c->srt_ctrl, 64 * 4, c->stream)) ||
+        (help && (st = reserve_zeroed(c->srt_help, kSortHelpWords * 8, c->stream))) ||
         (st = c->srt_items.reserve(cap * 20)))
         return st;
     // descriptors, then the fold values by slot
     uint8_t* const ib = c->srt_items.as<uint8_t>();
+    if (!c->sorted_users)
+    {
+        c->sorted_users = &d->sorted_users;
+        c->sorted_users->fetch_add(1);
+    }
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
                        reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
-                       sorted_lane_rows()};
+                       sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base,
+                       nullptr, 0, 0};
+    if (help)
+    {
+        if (++c->help_epoch == 0) c->help_epoch = 1;
+        ws.help = c->srt_help.as<uint64_t>();
+        ws.help_epoch = c->help_epoch;
+        ws.ring_base = c->ring_base;
+        c->ring_base += uint32_t(grid);  // every workgroup appends itself once
+    }
+    // MI_CRC32C_SORT_BARRIER_SKEW=1 (tests): the kernel waits for one arrival
+    // more than the grid has, so every workgroup's wait times out
+    const char* skew = std::getenv("MI_CRC32C_SORT_BARRIER_SKEW");
+    if (ws.fused && skew && !std::strcmp(skew, "1")) ws.bar_base += 1;
     HIP_TRY(launch_sorted(base, off, len, inits, count, ws, out, d->d_tables, d->d_pow2, grid,
                           c->stream));
+    c->bar_tag = ws.fused ? ws.bar_base + uint32_t(grid) + 1u : 0u;
+    if (ws.fused) c->bar_base += uint32_t(grid);
     c->sorted_ctrl = ws.ctrl;
-    mi_host::note_sorted_batch();
+    mi_host::note_sorted_batch(ws.fused != 0);
     return MI_CRC32C_OK;
 }
 
@@ -830,8 +895,9 @@ int mi_crc32c_stream_sync(void)
             HIP_TRY(hipStreamSynchronize(c->stream));
             mi_host::note_hint_overflow();
             return fail(MI_CRC32C_EINVAL,
-                        "an asynchronous batch's total_bytes hint understated the sum of its "
-                        "lengths: its out[] is incomplete");
+                        "an asynchronous sorted batch left out[] incomplete: its total_bytes "
+                        "hint understated the sum of its lengths, or its one-launch grid barrier "
+                        "timed out (another barrier launch held CUs)");
         }
     }
     return MI_CRC32C_OK;
@@ -894,11 +960,22 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         // (sorted path: a workgroup found no room for its descriptors; piece
         // path: the plan exceeded its capacity).  Then hash the batch again
         // with the plan size read back (total_bytes = 0): exact, slower.
-        uint32_t* flag = c->pin_small.as<uint32_t>() + 1;
-        HIP_TRY(hipMemcpyAsync(flag, c->sorted_ctrl ? c->sorted_ctrl + 1 : c->plan_total, 4,
-                               hipMemcpyDeviceToHost, c->stream));
+        uint32_t* flag = c->pin_small.as<uint32_t>() + 4;  // ctrl[0..3] / the plan total
+        HIP_TRY(hipMemcpyAsync(flag, c->sorted_ctrl ? c->sorted_ctrl : c->plan_total,
+                               c->sorted_ctrl ? 16 : 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        const bool overflow = c->sorted_ctrl ? *flag != 0 : *flag > c->plan_cap;
+        // the one-launch form's barrier timed out (ctrl[3] holds this launch's
+        // tag, bar_base after it + 1): hash the batch again with two launches
+        if (c->sorted_ctrl && c->bar_tag && flag[3] == c->bar_tag)
+        {
+            HIP_TRY(hipMemsetAsync(c->sorted_ctrl + 2, 0, 8, c->stream));
+            c->force_unfused = true;
+            if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out))) return st;
+            c->force_unfused = false;
+            HIP_TRY(hipMemcpyAsync(flag, c->sorted_ctrl, 16, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
+        const bool overflow = c->sorted_ctrl ? flag[1] != 0 : flag[0] > c->plan_cap;
         if (!overflow) return MI_CRC32C_OK;
         // the sticky word (ctrl[2]) is for asynchronous batches: this one is
         // recovered here.  With an unchecked asynchronous batch before it on

@@ -69,7 +69,7 @@ bool have_sse42()
 
 std::atomic<uint64_t> g_gpu_calls{0}, g_fb_calls{0}, g_fb_bytes{0}, g_sharded{0}, g_sorted{0},
     g_routed_calls{0}, g_routed_bytes{0}, g_zero_copy{0}, g_hint_overflow{0},
-    g_host_batches{0}, g_host_batch_bytes{0};
+    g_host_batches{0}, g_host_batch_bytes{0}, g_sorted_one{0};
 std::atomic<int> g_fb_status{0};
 std::atomic<int> g_multi_ranges{0};
 std::atomic<int> g_multi_devs[MI_CRC32C_MAX_DEVICES];
@@ -111,7 +111,11 @@ void note_fallback(int status, uint64_t bytes)
 
 void note_gpu_call() { g_gpu_calls.fetch_add(1, std::memory_order_relaxed); }
 void note_sharded_call() { g_sharded.fetch_add(1, std::memory_order_relaxed); }
-void note_sorted_batch() { g_sorted.fetch_add(1, std::memory_order_relaxed); }
+void note_sorted_batch(bool one_launch)
+{
+    g_sorted.fetch_add(1, std::memory_order_relaxed);
+    if (one_launch) g_sorted_one.fetch_add(1, std::memory_order_relaxed);
+}
 void note_zero_copy_batch() { g_zero_copy.fetch_add(1, std::memory_order_relaxed); }
 void note_hint_overflow() { g_hint_overflow.fetch_add(1, std::memory_order_relaxed); }
 void note_host_batch(uint64_t bytes)
@@ -149,6 +153,7 @@ void mi_crc32c_stats(mi_crc32c_stats_t* out)
     out->hint_overflows = mi_host::g_hint_overflow.load();
     out->host_batches = mi_host::g_host_batches.load();
     out->host_batch_bytes = mi_host::g_host_batch_bytes.load();
+    out->sorted_one_launch = mi_host::g_sorted_one.load();
     out->last_fallback_status = mi_host::g_fb_status.load();
     const int ranges = mi_host::g_multi_ranges.load();
     out->last_multi_ranges = ranges;
@@ -167,6 +172,7 @@ void mi_crc32c_stats_reset(void)
     mi_host::g_hint_overflow.store(0);
     mi_host::g_host_batches.store(0);
     mi_host::g_host_batch_bytes.store(0);
+    mi_host::g_sorted_one.store(0);
     mi_host::g_routed_calls.store(0);
     mi_host::g_routed_bytes.store(0);
     mi_host::g_fb_status.store(0);

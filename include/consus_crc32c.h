@@ -103,6 +103,7 @@ typedef struct mi_crc32c_stats_t
                                      (MI_CRC32C_CPU: durable-log flushes below the
                                      crossover) */
     uint64_t host_batch_bytes;    /* bytes of those batches */
+    uint64_t sorted_one_launch;   /* sorted batches hashed in one launch (grid barrier) */
 } mi_crc32c_stats_t;
 void mi_crc32c_stats(mi_crc32c_stats_t* out);
 void mi_crc32c_stats_reset(void);

@@ -9,7 +9,12 @@ piece ("auto", 4-row ring, whole records finished in the loop), with the
 also with lane items off (MI_CRC32C_SORT_LANE_ROWS=0: records of <= 2 rows
 take teams too).  MI_CRC32C_VARPATH=sorted makes the default explicit;
 every result is compared with the CPU oracle, bit-exact, and the path is
-checked to have run (mi_crc32c_stats().sorted_batches).
+checked to have run (mi_crc32c_stats().sorted_batches).  The hash kernel
+computes the cost blocks itself behind a grid barrier (one launch, round 5)
+with MI_CRC32C_SORT_FUSED=1 (the "one launch" parameter; measured slower than
+sorted_cost_kernel + the hash kernel, the default) while no other thread's
+context uses the sorted path on the device.  Lane items are helped across
+workgroups (MI_CRC32C_SORT_HELP, default on) in batches of >= 64K records.
 """
 import os
 
@@ -19,13 +24,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["auto", "auto-ring2", "16", "16-nolane"],
-                ids=["piece_auto", "piece_auto_ring2", "piece_64k", "piece_64k_teams_only"])
+@pytest.fixture(params=["auto", "auto-1launch", "auto-ring2", "16", "16-nolane", "16-help"],
+                ids=["piece_auto", "piece_auto_one_launch", "piece_auto_ring2", "piece_64k",
+                     "piece_64k_teams_only", "piece_64k_help_every_size"])
 def sorted_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
-    if request.param == "auto-ring2":
+    if request.param == "auto-1launch":
+        os.environ["MI_CRC32C_SORT_FUSED"] = "1"  # cost blocks + a grid barrier in the hash kernel
+    elif request.param == "auto-ring2":
         os.environ["MI_CRC32C_SORT_RING"] = "2"
+    elif request.param == "16-help":
+        os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = "16"
+        os.environ["MI_CRC32C_SORT_HELP"] = "2"  # lane items helped across workgroups
     elif request.param == "16-nolane":
         os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = "16"
         os.environ["MI_CRC32C_SORT_LANE_ROWS"] = "0"
@@ -36,6 +47,8 @@ def sorted_path(engine, request):
     os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
     os.environ.pop("MI_CRC32C_SORT_RING", None)
     os.environ.pop("MI_CRC32C_SORT_LANE_ROWS", None)
+    os.environ.pop("MI_CRC32C_SORT_FUSED", None)
+    os.environ.pop("MI_CRC32C_SORT_HELP", None)
     if old is None:
         del os.environ["MI_CRC32C_VARPATH"]
     else:
@@ -434,3 +447,109 @@ def test_sorted_descriptor_staging_limits(engine, oracle, sorted_path, count):
                               oracle.batch(buf, offsets, lengths, inits))
     finally:
         del os.environ["MI_CRC32C_SORTED_GRID"]
+
+
+def test_sorted_one_launch_runs_and_matches_two_launches(engine, oracle):
+    """The one-launch form (cost blocks and a grid barrier in the hash
+    kernel) runs when this thread's context is the only sorted one, and gives
+    the same CRCs as the two-launch form, on configs[2]-distributed records
+    with inits, split records and 0-3 B records."""
+    rng = np.random.default_rng(77)
+    count = 50_000
+    lengths = engine.zipf_lengths(0x5EED, count).astype(np.uint32)
+    lengths[rng.integers(0, count, 500)] = rng.integers(0, 4, 500)
+    lengths[rng.integers(0, count, 20)] = rng.integers(70_000, 300_000, 20)
+    offsets, end = _packed(rng, lengths, start=3)
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32)
+    want = oracle.batch(buf, offsets, lengths, inits)
+    os.environ["MI_CRC32C_VARPATH"] = "sorted"
+    try:
+        for plog in ("16", "12"):
+            os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = plog
+            os.environ["MI_CRC32C_SORT_FUSED"] = "1"
+            before = engine.stats()["sorted_one_launch"]
+            assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits), want), plog
+            assert engine.stats()["sorted_one_launch"] - before == 1, plog
+            os.environ["MI_CRC32C_SORT_FUSED"] = "0"
+            before = engine.stats()["sorted_one_launch"]
+            assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits), want), plog
+            assert engine.stats()["sorted_one_launch"] == before, plog
+            del os.environ["MI_CRC32C_SORT_FUSED"]
+    finally:
+        for k in ("MI_CRC32C_VARPATH", "MI_CRC32C_SORT_PIECE_LOG2", "MI_CRC32C_SORT_FUSED"):
+            os.environ.pop(k, None)
+
+
+def test_sorted_one_launch_barrier_timeout_recovers(engine, oracle):
+    """The grid barrier's wait is bounded: with MI_CRC32C_SORT_BARRIER_SKEW=1
+    every workgroup waits for one arrival too many, times out (50 ms), tags
+    ctrl[3] and returns.  A synchronous batch then recomputes with two
+    launches (exact); an asynchronous one is reported by the next stream
+    sync (EINVAL), after which the engine is clean."""
+    rng = np.random.default_rng(78)
+    count = 8_000
+    lengths = engine.zipf_lengths(0x5EEE, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    want = oracle.batch(buf, offsets, lengths)
+    os.environ["MI_CRC32C_VARPATH"] = "sorted"
+    os.environ["MI_CRC32C_SORT_BARRIER_SKEW"] = "1"
+    os.environ["MI_CRC32C_SORT_FUSED"] = "1"
+    try:
+        assert np.array_equal(_device_run(engine, buf, offsets, lengths), want)
+        data = engine.DeviceBuffer(buf.size)
+        data.upload(buf)
+        d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                               engine.DeviceBuffer(count * 4))
+        d_off.upload(offsets)
+        d_len.upload(lengths)
+        engine.device_batch(data, d_off, d_len, count, d_out,
+                            total_bytes=int(lengths.sum(dtype=np.uint64)), asynchronous=True)
+        with pytest.raises(engine.EngineError):
+            engine.sync()
+        del os.environ["MI_CRC32C_SORT_BARRIER_SKEW"]
+        engine.sync()
+        engine.device_batch(data, d_off, d_len, count, d_out,
+                            total_bytes=int(lengths.sum(dtype=np.uint64)), asynchronous=True)
+        engine.sync()
+        assert np.array_equal(d_out.download(np.uint32, count), want)
+        for b in (data, d_off, d_len, d_out):
+            b.free()
+    finally:
+        for k in ("MI_CRC32C_VARPATH", "MI_CRC32C_SORT_BARRIER_SKEW", "MI_CRC32C_SORT_FUSED"):
+            os.environ.pop(k, None)
+
+
+@pytest.mark.parametrize("grid", [None, "7", "40"])
+def test_sorted_lane_help_across_workgroups(engine, oracle, grid):
+    """Lane items (records of <= 2 rows) are published by each workgroup when
+    its first wave finishes its team groups and drained by atomic claims on
+    its cursor, by its own waves and by the waves of workgroups that are
+    done.  Each item must be hashed exactly
+    once: a 120K-record batch, most of it lane items, with inits, split
+    records and 0-3 B records, at the default grid and small ones (a few
+    workgroups with many items each), help forced on, against the oracle and
+    against help off."""
+    rng = np.random.default_rng(91)
+    count = 120_000
+    lengths = rng.integers(4, 300, count).astype(np.uint32)
+    big = rng.integers(0, count, 3000)
+    lengths[big] = engine.zipf_lengths(0x1234, 3000)
+    lengths[rng.integers(0, count, 30)] = rng.integers(70_000, 200_000, 30)
+    lengths[rng.integers(0, count, 500)] = rng.integers(0, 4, 500)
+    offsets, end = _packed(rng, lengths, gap=3, start=5)
+    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32)
+    want = oracle.batch(buf, offsets, lengths, inits)
+    os.environ["MI_CRC32C_VARPATH"] = "sorted"
+    if grid:
+        os.environ["MI_CRC32C_SORTED_GRID"] = grid
+    try:
+        for mode in ("2", "0", "2"):
+            os.environ["MI_CRC32C_SORT_HELP"] = mode
+            got = _device_run(engine, buf, offsets, lengths, inits)
+            assert np.array_equal(got, want), (grid, mode, int(np.sum(got != want)))
+    finally:
+        for k in ("MI_CRC32C_VARPATH", "MI_CRC32C_SORTED_GRID", "MI_CRC32C_SORT_HELP"):
+            os.environ.pop(k, None)

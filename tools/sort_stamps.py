@@ -66,3 +66,36 @@ if last == 7:
           f"max {fin.max():.2f}")
 print("per XCD group (workgroup % 8): median workgroup end " +
       " ".join(f"{np.median(wg_end[x::8]):.1f}" for x in range(8)))
+
+
+def ends_of_next(k):
+    """Team-phase ends per workgroup (us after that launch's start) of k more
+    single batches, each read back after its own sync."""
+    res = []
+    for _ in range(k):
+        E.device_batch(data, d_off, d_len, R, out, total_bytes=hint, asynchronous=True)
+        E.sync()
+        s2 = np.zeros(256 * 16 * 8, dtype=np.uint64)
+        assert lib.mi_debug_sort_stamps(s2.ctypes.data, s2.size) == 0
+        s2 = s2.reshape(256, 16, 8).astype(np.int64)
+        u2 = (s2 - s2[:, :, 0].min()) / 100.0
+        res.append(u2[:, :, 5].max(axis=1))
+    return res
+
+
+# Is a workgroup's speed a property of where it runs (the same workgroups slow
+# launch after launch), or noise?  Correlation of the per-workgroup team-phase
+# ends of consecutive launches (the shares are the same batch's).
+if "--repeat" in sys.argv:
+    k = int(sys.argv[sys.argv.index("--repeat") + 1])
+    ends = [team_end] + ends_of_next(k)
+    m = np.array(ends)
+    dev = m - m.mean(axis=1, keepdims=True)
+    c = np.corrcoef(dev)
+    print(f"team-end spread per launch (max - min, us): " + " ".join(f"{x.max() - x.min():.1f}" for x in m))
+    print(f"correlation of per-workgroup team ends between launches: min {c[np.triu_indices(len(m), 1)].min():.3f} "
+          f"mean {c[np.triu_indices(len(m), 1)].mean():.3f}")
+    avg = dev.mean(axis=0)
+    print(f"per-workgroup mean deviation over launches: sd {avg.std():.2f} us, per-launch residual sd "
+          f"{(dev - avg).std():.2f} us")
+    print("per XCD group mean deviation: " + " ".join(f"{avg[x::8].mean():+.1f}" for x in range(8)))
