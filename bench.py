@@ -511,24 +511,33 @@ def run_dlog(args, compact: bool = False) -> dict:
         res["gpu_vs"] = {name: versus(eng["gpu"], eng[name]) for name, _ in engines if name != "gpu"}
         best = median_run(runs[wname]["gpu"])
         pf = per_flush(best)
-        # the per-flush bound: the cheaper of the GPU batch's floor (a one-frame
-        # round trip through the log's entry point, measured by dlog_bench, plus
-        # the bytes at the host link's ~55 GB/s) and the flush thread's CPU
-        # path at this size (measured in the same process); the log routes
-        # each flush to one of the two by its size (durable_log.cc)
+        # The per-flush bound: the cheaper of the two routes the log chooses
+        # between by size (durable_log.cc host_batch_max).  The GPU batch's:
+        # its floor (a one-frame round trip through the log's entry point,
+        # measured by dlog_bench) plus the bytes at the host link's ~55 GB/s.
+        # The flush thread's CPU: the reference crc32c.cc engine's own time
+        # per byte on the flush thread in the same job (the same frames, just
+        # written by the appenders on other cores), at this flush's size.  The
+        # CPU loop on a warm buffer (cpu_batch_us_at_flush, dlog_bench) is
+        # reported beside it: flushed frames are not in this core's cache.
         nb = pf["frame_bytes_per_flush"]
         gpu_bound = best.get("empty_batch_us", 0.0) + nb / 55e3
         cpu_us = _interp(best.get("cpu_batch_us", {}), nb)
-        bound = min(gpu_bound, cpu_us) if cpu_us else gpu_bound
-        pf.update({"empty_batch_us": best.get("empty_batch_us", 0.0),
-                   "gpu_batch_bound_us": round(gpu_bound, 2),
-                   "cpu_batch_us_at_flush": None if cpu_us is None else round(cpu_us, 2),
-                   "batch_crc_bound_us": round(bound, 2),
-                   "batch_crc_vs_bound": round(pf["us_per_flush"]["batch_crc"] / bound, 3)})
+        ref_us = None
         if "reference-cpu" in runs[wname]:
             rc = per_flush(median_run(runs[wname]["reference-cpu"]))
             pf["reference_cpu_us_per_flush"] = rc["us_per_flush"]["batch_crc"]
             pf["reference_cpu_frame_bytes_per_flush"] = rc["frame_bytes_per_flush"]
+            if rc["frame_bytes_per_flush"]:
+                ref_us = rc["us_per_flush"]["batch_crc"] * nb / rc["frame_bytes_per_flush"]
+        bound = min(gpu_bound, ref_us) if ref_us else gpu_bound
+        pf.update({"empty_batch_us": best.get("empty_batch_us", 0.0),
+                   "gpu_batch_bound_us": round(gpu_bound, 2),
+                   "reference_cpu_us_at_flush": None if ref_us is None else round(ref_us, 2),
+                   "cpu_batch_us_at_flush": None if cpu_us is None else round(cpu_us, 2),
+                   "batch_crc_bound_us": round(bound, 2),
+                   "batch_crc_vs_bound": round(pf["us_per_flush"]["batch_crc"] / bound, 3),
+                   "routed_to_cpu": f"{pf['host_flushes']} of {pf['flushes']} flushes"})
         res["flush"] = pf
         if not compact:
             res["runs_detail"] = runs[wname]
@@ -980,8 +989,12 @@ def main():
         for key, cfg in (("config2_zipf", "zipf"), ("config4_stream", "stream"),
                          ("config1_pcie_inclusive", "pcie4k")):
             # the zipf leg warms up for >= 100 steps (~80 ms): it starts after host-side
-            # preparation with the GPU idle, and 5 steps leave it in the clock ramp
-            sub = sub_args(args, cfg, **({"warmup": max(args.warmup, 100)} if cfg == "zipf" else {}))
+            # preparation with the GPU idle, and 5 steps leave it in the clock ramp;
+            # it times >= 100 steps (~77 ms, sync-bracketed), since in a 20-step window
+            # (15 ms) the restart after the warm-up's sync costs ~6 us a step
+            # (round 5, profiles/r05_zipf_leg_window.txt)
+            sub = sub_args(args, cfg, **({"warmup": max(args.warmup, 100), "steps": max(args.steps, 100)}
+                                         if cfg == "zipf" else {}))
             progress(f"PMC traffic pass ({cfg})")
             legs.append((key, sub, pmc_traffic(sub) if not args.no_pmc else (None, "skipped")))
         # the durable-log front-end: appends/s and the per-flush

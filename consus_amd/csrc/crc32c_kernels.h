@@ -141,16 +141,7 @@ struct SortedWorkspace
     // ctrl[32] counts arrivals, bar_base = its value before this launch.
     int fused;
     uint32_t bar_base;
-    // Cross-workgroup help with lane items (round 5; null: off): the
-    // workspace of kSortHelpWords words, zeroed once; this launch's tag
-    // (never 0) and the ring counter's value before it.
-    uint64_t* help;
-    uint32_t help_epoch;
-    uint32_t ring_base;
 };
-constexpr uint32_t kSortHelpMaxGrid = 1024;
-constexpr uint64_t kSortHelpWords = 16 + kSortHelpMaxGrid + 8 * uint64_t(kSortHelpMaxGrid);
-constexpr uint64_t kSortHelpMinCount = 1u << 16;  // records: smaller batches do not help (engine)
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);
 constexpr uint32_t kSortPieceLog2 = 16;  // 64 KiB pieces (the default)

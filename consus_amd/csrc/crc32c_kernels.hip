@@ -88,6 +88,50 @@ __device__ __forceinline__ void stage_tables(const uint32_t* __restrict__ g)
     __syncthreads();
 }
 
+// The same staging in two halves (the sorted kernel, round 5): the loads
+// issued early into registers, the LDS stores later, so the L2 round trip
+// overlaps the work between them.
+struct TableRegs
+{
+    uint32_t v[1024u * 8u / kBlock];
+    uint4 t[((4096u + 2048u) / 4u + kBlock - 1) / kBlock];
+};
+__device__ __forceinline__ void load_tables(TableRegs& R, const uint32_t* __restrict__ g)
+{
+    constexpr uint32_t NM = 1024u * 8u / kBlock, NT = (4096u + 2048u) / 4u;
+    constexpr uint32_t NTI = (NT + kBlock - 1) / kBlock;
+    const uint4* src = reinterpret_cast<const uint4*>(g + kTabT);
+#pragma unroll
+    for (uint32_t k = 0; k < NM; ++k) R.v[k] = g[kTabMain + ((threadIdx.x + k * kBlock) >> 3)];
+#pragma unroll
+    for (uint32_t k = 0; k < NTI; ++k)
+    {
+        const uint32_t i = threadIdx.x + k * kBlock;
+        R.t[k] = i < NT ? src[i] : make_uint4(0, 0, 0, 0);
+    }
+}
+__device__ __forceinline__ void store_tables(const TableRegs& R)
+{
+    constexpr uint32_t NM = 1024u * 8u / kBlock, NT = (4096u + 2048u) / 4u;
+    constexpr uint32_t NTI = (NT + kBlock - 1) / kBlock;
+#pragma unroll
+    for (uint32_t k = 0; k < NM; ++k)
+    {
+        const uint32_t i = threadIdx.x + k * kBlock;
+        const uint32_t e = i >> 3, c4 = (i & 7u) * 4u, tb = e >> 8, b = e & 255u;
+        const uint32_t addr = (tb >> 1) * 65536u + b * 256u + (tb & 1u) * 128u + c4 * 4u;
+        *reinterpret_cast<uint4*>(smem + kLdsMain + addr) = make_uint4(R.v[k], R.v[k], R.v[k], R.v[k]);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(smem + kLdsT);
+#pragma unroll
+    for (uint32_t k = 0; k < NTI; ++k)
+    {
+        const uint32_t i = threadIdx.x + k * kBlock;
+        if (i < NT) dst[i] = R.t[k];
+    }
+    __syncthreads();
+}
+
 // Lane info for the v_perm address builder: byte0 = c*4, byte1 = c*4 + 128,
 // byte2 = 0, byte3 = 1 (the 64 KiB half for tables 2 and 3).
 __device__ __forceinline__ uint32_t lane_info()
@@ -2038,10 +2082,7 @@ struct SortShared
     uint32_t n_full;           // full pieces (listed first: the largest items)
     uint32_t full_base;        // their slots: items[count + full_base ...]
     uint32_t next_group;
-    uint32_t next_lane;        // lane items taken (64 per grab; without help)
-    uint32_t teams_done;       // waves past their team groups (the first publishes)
-    uint32_t help_arrived;     // waves at the help phase (the first polls the ring)
-    uint32_t help_word;        // the poller's announcement: gen << 12 | victim; ~0: done
+    uint32_t next_lane;        // lane items taken (64 per grab)
     uint32_t lane_base;        // the first lane item's position among the last pieces
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
@@ -2446,6 +2487,9 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #ifndef MI_SORT_LANE_BLOCKS
 #define MI_SORT_LANE_BLOCKS 16
 #endif
+#ifndef MI_SORT_TABLE_EARLY
+#define MI_SORT_TABLE_EARLY 0
+#endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 #define SORT_STAMP(k)                                                                        \
@@ -2469,8 +2513,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
-    uint32_t lrows, int fused, uint32_t bar_base, uint64_t* __restrict__ help, uint32_t help_epoch,
-    uint32_t ring_base)
+    uint32_t lrows, int fused, uint32_t bar_base)
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint64_t piece = uint64_t(1) << plog;
@@ -2480,29 +2523,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     if (threadIdx.x == 0) S.next_lane = 0;
-    if (threadIdx.x == 0) S.teams_done = S.help_arrived = S.help_word = 0;
-    // Help with lane items across workgroups (DESIGN.md section 4.7, round
-    // 5): the help workspace H holds the ring counter (word 0), the ring of
-    // published workgroups (words 16 ..), and per workgroup v its record at
-    // word 16 + kSortHelpMaxGrid + 8 v: two granules {tag, lane items} and
-    // {tag, list start}, then its lane cursor.
-    const bool helping = help && gridDim.x > 1 && gridDim.x <= kSortHelpMaxGrid;
-    auto pubA = [&](uint32_t v) { return help + 16 + kSortHelpMaxGrid + 8 * uint64_t(v); };
-    auto curp = [&](uint32_t v) { return reinterpret_cast<uint32_t*>(pubA(v) + 2); };
-    // every workgroup appends itself to the ring exactly once per launch (the
-    // host advances ring_base by the grid), with its lane list or none
-    auto publish = [&](uint32_t n_lane, uint32_t list_start) {
-        __hip_atomic_store(pubA(blockIdx.x), (uint64_t(help_epoch) << 32) | n_lane, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(pubA(blockIdx.x) + 1, (uint64_t(help_epoch) << 32) | list_start,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the granules before the ring entry
-        const uint32_t k = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(help), 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) - ring_base;
-        if (k < kSortHelpMaxGrid)
-            __hip_atomic_store(help + 16 + k, (uint64_t(help_epoch) << 32) | blockIdx.x, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    };
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
     // whole records finished in the loop (RB = 4, small batches) or by the
@@ -2510,15 +2530,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // ms against 0.788-0.791, profiles/r04_configs2_variants_ab.txt)
     constexpr bool INLOOP = RB >= 4;
     if (INLOOP) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
-    // (1) Wave 0: the two targets and the cost blocks holding them, while the
-    // other waves stage the tables (the staging's barrier covers both).
+    // (1) Wave 0: the two targets and the cost blocks holding them.  (The
+    // tables are staged later, at the stage_tables() call after the binning
+    // has written the descriptor list out: until then their LDS holds the
+    // list, so no table lookup may come before that call.)
     SORT_STAMP(0);
     if (fused && !sorted_fused_costs(base, off, len, inits, count, blk_cost, nb, ctrl, out, tables,
                                      plog, bar_base, S))
-    {
-        if (helping && threadIdx.x == 0) publish(0, 0);
         return;  // the grid barrier timed out: ctrl[3] tells the host (below)
-    }
     if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
     __syncthreads();
     SORT_STAMP(1);
@@ -2590,16 +2609,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     auto put = [&](uint4* dst, const uint4& dv) {
         __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
     };
-    // Lane-item descriptors, when other workgroups may help with them:
-    // write-through (sc1) stores, which other CUs read with sc1 loads without
-    // a release/acquire pair (MI355X_MICROARCH.md, inter-workgroup visibility)
-    auto put_shared = [&](uint4* dst, const uint4& dv) {
-        uint64_t* const q = reinterpret_cast<uint64_t*>(dst);
-        __hip_atomic_store(q, uint64_t(dv.x) | (uint64_t(dv.y) << 32), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(q + 1, uint64_t(dv.z) | (uint64_t(dv.w) << 32), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    };
     // Up to kLdsBytes / 16 items, the descriptors go to LDS at their list
     // position (the table image's space: the tables are staged after), and
     // then out in list order, whole lines: scattered 16-B stores cost the
@@ -2613,7 +2622,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     auto put_last = [&](uint32_t pos, const uint4& dv) {
         if (staged) stage_lds[stage_nf + pos] = dv;
-        else if (helping && pos >= S.lane_base) put_shared(lastv + pos, dv);
         else put(lastv + pos, dv);
     };
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
@@ -2659,6 +2667,13 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         }
     };
     pass(false);
+#if MI_SORT_TABLE_EARLY
+    // the table image's loads now, its LDS stores after the descriptor list
+    // has left the LDS (round 5): their L2 round trip overlaps the bin scan,
+    // the placement and the copy-out
+    TableRegs treg;
+    load_tables(treg, tables);
+#endif
     __syncthreads();
     SORT_STAMP(3);
     {
@@ -2720,33 +2735,20 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         else
             pass(true);
     }
-    if (helping) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (helpers read lane descriptors)
     __syncthreads();
-    if (n_items == 0)
-    {
-        if (helping && threadIdx.x == 0) publish(0, 0);
-        return;
-    }
-    if (helping && threadIdx.x == 0)
-    {
-        __hip_atomic_store(curp(blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (n_items == 0) return;
     if (staged)
     {
         // list order out: full pieces to their region, the rest after rlo
         for (uint32_t i = threadIdx.x; i < n_items; i += kBlock)
-        {
-            uint4* const dst = i < n_full ? fullv + S.full_base + i : lastv + (i - n_full);
-            if (helping && i >= n_full + S.lane_base)
-                put_shared(dst, stage_lds[i]);  // a lane item: helpers read it
-            else
-                put(dst, stage_lds[i]);
-        }
-        if (helping) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
         __syncthreads();
     }
+#if MI_SORT_TABLE_EARLY
+    store_tables(treg);  // ends with a barrier
+#else
     stage_tables(tables);  // ends with a barrier
+#endif
     SORT_STAMP(4);
     // team items first, lane items (positions n_long ..) after them
     const uint32_t n_long = n_full + S.lane_base;
@@ -2844,26 +2846,19 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // finish.  The list is ordered by block count, so the lanes of a wave run
     // about the same number of steps.  Blocks are read with the default
     // policy: a block's line is shared with the neighbouring records.
-    // One list of lane items: this workgroup's (cur: its global cursor when
-    // helping, else null: the LDS counter) or a victim's (its cursor).
     // blocks of one lane item loaded at once (a multiple of 4; the rest of a
     // longer item takes another round)
     constexpr int32_t kLaneBlocks = MI_SORT_LANE_BLOCKS;
-    auto lane_items = [&](const uint4* listLane, uint32_t n_lane, uint32_t* cur) __attribute__((always_inline)) {
+    auto lane_items = [&]() {
+        const uint32_t n_lane = n_items - n_long;
+        const uint4* const listLane = listL + n_long;
         auto grab64 = [&]() {
             uint32_t c = 0;
-            if (lane == 0)
-                c = cur ? __hip_atomic_fetch_add(cur, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : atomicAdd(&S.next_lane, 64u);
+            if (lane == 0) c = atomicAdd(&S.next_lane, 64u);
             return uint32_t(__builtin_amdgcn_readfirstlane(int(c)));
         };
         auto ldesc = [&](uint32_t c) {
-            if (c + lane >= n_lane) return make_uint4(0, 0, 0, 0);
-            if (!cur) return listLane[c + lane];
-            const uint64_t* q = reinterpret_cast<const uint64_t*>(listLane + c + lane);
-            const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
+            return c + lane < n_lane ? listLane[c + lane] : make_uint4(0, 0, 0, 0);
         };
         // Latency (round 5): a grab used to be three dependent global round
         // trips or more (its descriptors, then its blocks four at a time,
@@ -3127,22 +3122,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     flush();
 
     SORT_STAMP(5);
-    const uint32_t n_lane_own = n_items - n_long;
-    if (helping)
-    {
-        // the first wave past its team groups publishes the lane list: its
-        // descriptors went out write-through (sc1) and every wave drained
-        // them (vmcnt(0)) before the prologue's barriers; the granules and
-        // the ring entry follow (helpers read everything with sc1 loads)
-        uint32_t ord = 0;
-        if (lane == 0) ord = atomicAdd(&S.teams_done, 1u);
-        ord = uint32_t(__builtin_amdgcn_readfirstlane(int(ord)));
-        if (ord == 0 && lane == 0) publish(n_lane_own, uint32_t(rlo - n_full + n_long));
-    }
-    lane_items(listL + n_long, n_lane_own, helping ? curp(blockIdx.x) : nullptr);
+    lane_items();
     SORT_STAMP(6);
-    if (!INLOOP)
-    {
+    if (INLOOP) return;  // whole records were finished in the loop
     // Finish pass, in list order (round 5): a whole record's fold value W
     // (wr at its slot, eight consecutive words per group) is Z_m(raw) of its
     // bytes, m = ceil128(E) - E; crc = ~Z_{-m}(W).  The team items past the
@@ -3185,88 +3167,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             if (!(dv[u].w & kSortMulti)) out[dv[u].w & kSortRecMask] = ~v;
         }
     }
-    }  // !INLOOP
     SORT_STAMP(7);
-    if (!helping) return;
-    // Help phase: this workgroup is done; its waves take lane items of the
-    // workgroups still running (the slowest publish last).  The first wave
-    // here polls the ring; when an entry names a workgroup with lane items
-    // left, it announces it in LDS and every wave here drains that list
-    // through its cursor (claims are atomic: each item is hashed once, by its
-    // owner or a helper).  Bounded: the poller stops once every workgroup has
-    // published and been examined, or after kSortHelpTicks.
-    constexpr uint64_t kSortHelpTicks = 3000;  // 30 us
-    auto steal = [&](uint32_t v) {
-        const uint64_t ga = __hip_atomic_load(pubA(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t gb = __hip_atomic_load(pubA(v) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((ga >> 32) != help_epoch || (gb >> 32) != help_epoch) return;
-        lane_items(items + uint32_t(gb), uint32_t(ga), curp(v));
-    };
-    uint32_t ord = 0;
-    if (lane == 0) ord = atomicAdd(&S.help_arrived, 1u);
-    ord = uint32_t(__builtin_amdgcn_readfirstlane(int(ord)));
-    const uint32_t G = gridDim.x;
-    if (ord == 0)
-    {
-        uint32_t pos = 0, gen = 0;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;)
-        {
-            const uint32_t avail = min(__hip_atomic_load(reinterpret_cast<uint32_t*>(help), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT) - ring_base, G);
-            if (pos < avail)
-            {
-                const uint32_t i = pos + lane;
-                const bool in = i < avail;
-                const uint64_t e = in ? __hip_atomic_load(help + 16 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : 0;
-                const bool valid = in && (e >> 32) == help_epoch;
-                // the valid prefix (an entry is stored just after its slot is taken)
-                const uint64_t bad = __builtin_amdgcn_ballot_w64(in && !valid);
-                const uint32_t nvalid = bad ? uint32_t(__builtin_ctzll(bad)) : min(avail - pos, 64u);
-                const uint32_t v = uint32_t(e);
-                const bool look = valid && lane < nvalid && v != blockIdx.x;
-                const uint64_t ga = look ? __hip_atomic_load(pubA(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-                const uint32_t cu = look ? __hip_atomic_load(curp(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-                uint64_t wm = __builtin_amdgcn_ballot_w64(look && (ga >> 32) == help_epoch && cu < uint32_t(ga));
-                while (wm)
-                {
-                    const int k = __builtin_ctzll(wm);
-                    wm &= wm - 1;
-                    const uint32_t vk = uint32_t(__builtin_amdgcn_readlane(int(v), k));
-                    ++gen;
-                    if (lane == 0)
-                        __hip_atomic_store(&S.help_word, (gen << 12) | vk, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    steal(vk);
-                }
-                pos += nvalid;
-                if (nvalid == 0) __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
-            if (avail >= G) break;  // every workgroup published and was examined
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kSortHelpTicks) break;
-            __builtin_amdgcn_s_sleep(16);
-        }
-        if (lane == 0)
-            __hip_atomic_store(&S.help_word, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    else
-    {
-        uint32_t seen = 0;
-        for (;;)
-        {
-            const uint32_t w = __hip_atomic_load(&S.help_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (w == 0xFFFFFFFFu) break;
-            if ((w >> 12) != seen)
-            {
-                seen = w >> 12;
-                steal(w & 0xFFFu);
-                continue;
-            }
-            __builtin_amdgcn_s_sleep(4);
-        }
-    }
 }
 
 #if MI_SORT_STAMP
@@ -3302,8 +3203,7 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base, ws.help, ws.help_epoch,
-                       ws.ring_base);
+                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base);
     return hipGetLastError();
 }
 

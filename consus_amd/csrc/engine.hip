@@ -331,7 +331,6 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
-    DevBuf srt_help;                       // its cross-workgroup lane help (zeroed once)
     DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
     uint32_t done_seq = 0;
     PinBuf pin_small;                   // plan-size read-back; word kDoneWord: completion word
@@ -349,8 +348,6 @@ struct Ctx
     std::atomic<int>* sorted_users = nullptr;
     uint32_t bar_base = 0;
     bool force_unfused = false;  // the retry after a timed-out barrier
-    uint32_t help_epoch = 0;     // the last help tag used (never 0)
-    uint32_t ring_base = 0;      // the help ring counter before the next launch
     uint32_t bar_tag = 0;        // ctrl[3] if the last one-launch batch's barrier timed out
     uint32_t* plan_total = nullptr;
     uint64_t plan_cap = 0;
@@ -425,7 +422,7 @@ struct Ctx
         sorted_users = nullptr;
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs, &srt_cost,
-                          &srt_ctrl, &srt_items, &srt_help, &done_ctr})
+                          &srt_ctrl, &srt_items, &done_ctr})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -661,17 +658,6 @@ bool fused_ok(DeviceState* d, const Ctx* c, int grid)
     return grid <= d->cus && d->sorted_users.load() == 1;
 }
 
-// Cross-workgroup help with lane items (crc32c_kernels.hip, the help phase),
-// for batches of at least kSortHelpMinCount records: MI_CRC32C_SORT_HELP=0
-// turns it off, =2 on at every size (A/B, tests; read per batch).
-bool sorted_help_on(uint64_t count)
-{
-    const char* e = std::getenv("MI_CRC32C_SORT_HELP");
-    if (e && !std::strcmp(e, "0")) return false;
-    if (e && !std::strcmp(e, "2")) return true;
-    return count >= kSortHelpMinCount;
-}
-
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
 int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
@@ -686,10 +672,8 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
         grid = std::max(1, std::min(8 * grid, std::atoi(e)));
     const uint64_t cap = sorted_item_cap(count, total_bytes, plog, grid);
     int st;
-    const bool help = sorted_help_on(count) && grid > 1 && grid <= int(kSortHelpMaxGrid);
     if ((st = c->srt_cost.reserve(uint64_t(sorted_blocks(count)) * 8)) ||
         (st = reserve_zeroed(c->srt_ctrl, 64 * 4, c->stream)) ||
-        (help && (st = reserve_zeroed(c->srt_help, kSortHelpWords * 8, c->stream))) ||
         (st = c->srt_items.reserve(cap * 20)))
         return st;
     // descriptors, then the fold values by slot
@@ -702,16 +686,7 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
                        reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
-                       sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base,
-                       nullptr, 0, 0};
-    if (help)
-    {
-        if (++c->help_epoch == 0) c->help_epoch = 1;
-        ws.help = c->srt_help.as<uint64_t>();
-        ws.help_epoch = c->help_epoch;
-        ws.ring_base = c->ring_base;
-        c->ring_base += uint32_t(grid);  // every workgroup appends itself once
-    }
+                       sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base};
     // MI_CRC32C_SORT_BARRIER_SKEW=1 (tests): the kernel waits for one arrival
     // more than the grid has, so every workgroup's wait times out
     const char* skew = std::getenv("MI_CRC32C_SORT_BARRIER_SKEW");

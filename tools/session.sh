@@ -107,12 +107,11 @@ while [ $# -gt 0 ]; do
     gpusorted) run pytest_sorted 900 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_parity.py tests/test_gpu_errors.py tests/test_gpu_direct.py -x -q --timeout 120 --timeout-method thread ;;
     stamps) for m in ${STAMP_MIB:-0 256 1}; do echo "== mib $m"; timeout -k 10 120 python3 tools/sort_stamps.py tools/ab/libconsus_crc32c_${STAMP_LIB:-stamp}.so --mib $m ${STAMP_ARGS:-} || exit 1; done | tee "$OUT/stamps.out" ;;
     zipffused) for rnd in 1 2 3; do for fz in 1 0; do echo -n "round $rnd fused=$fz "; MI_CRC32C_SORT_FUSED=$fz timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"; done; done | tee "$OUT/zipffused.out" ;;
-    zipfhelp) for rnd in 1 2 3; do for hp in 1 0; do echo -n "round $rnd help=$hp "; MI_CRC32C_SORT_HELP=$hp timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"; done; done | tee "$OUT/zipfhelp.out" ;;
-    midhelp) for hp in 1 0; do MI_CRC32C_SORT_HELP=$hp run mid_help$hp 300 python3 -u tools/mid_probe.py --path sorted --mib ${MID_MIB:-1,16,64,256,1024} --reps 100 || exit 1; done ;;
-    legcmp) for rnd in 1 2; do
-               echo -n "round $rnd bench --config zipf: "; timeout -k 10 200 python3 bench.py --config zipf --steps 20 --warmup 100 --no-cpu --no-pmc --leg-sustain-seconds 1 > "$OUT/lc.out" 2>"$OUT/lc.err" || { tail -5 "$OUT/lc.err"; exit 1; }
+    legcmp) for rnd in 1 2; do for k in 20 100; do
+               echo -n "round $rnd bench --config zipf --steps $k (ms_per_step, events, sustained, digest): "; timeout -k 10 200 python3 bench.py --config zipf --steps $k --warmup 100 --no-cpu --no-pmc --leg-sustain-seconds 1 > "$OUT/lc.out" 2>"$OUT/lc.err" || { tail -5 "$OUT/lc.err"; exit 1; }
                python3 -c "import json,sys; r=json.loads(open('$OUT/lc.out').read().strip().splitlines()[-1]); print(r['ms_per_step'], r['roofline']['step_ms_events'], r['sustained']['step_ms'], r['digest_verified'])"
-               echo -n "round $rnd zipf_probe: "; timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done
+             echo -n "round $rnd zipf_probe: "; timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
              done | tee "$OUT/legcmp.out" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
