@@ -113,6 +113,9 @@ while [ $# -gt 0 ]; do
              done
              echo -n "round $rnd zipf_probe: "; timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
              done | tee "$OUT/legcmp.out" ;;
+    earlyab) for rnd in 1 2 3; do for cfg in ${EARLY_CFGS:-"r05d 0" "lb8 0" "lb8 2" "lb8 4" "lb8 8"}; do
+               set -- $cfg; echo -n "round $rnd lib=$1 lane_early=$2 "; MI_CRC32C_SORT_LANE_EARLY=$2 timeout -k 10 120 python3 tools/zipf_probe.py tools/ab/libconsus_crc32c_$1.so > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done; done | tee "$OUT/earlyab.out" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
