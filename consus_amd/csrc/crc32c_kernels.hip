@@ -2444,6 +2444,9 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #ifndef MI_SORT_LANE_BLOCKS
 #define MI_SORT_LANE_BLOCKS 16
 #endif
+#ifndef MI_SORT_LANE_EARLY
+#define MI_SORT_LANE_EARLY 0
+#endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 #define SORT_STAMP(k)                                                                        \
@@ -2633,7 +2636,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const uint32_t e = uint32_t(block_excl_scan64(c, S.wsum, total));
         if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = e;
         if (threadIdx.x == kSortRows - lrows) S.lane_base = e;  // lane items follow the team items
+#if MI_SORT_LANE_EARLY
         if (early_waves && threadIdx.x == kSortRows - early_rows) S.small_base = e;
+#endif
         if (threadIdx.x == 0)
         {
             // full pieces go to this workgroup's own region of fpw slots
@@ -2917,11 +2922,19 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // items (LDS-bound) beside the other waves' small groups (latency-bound),
     // then return to the groups that are left.  The other waves go to the lane
     // items when the groups run out, as before.
+    // Compiled in with MI_SORT_LANE_EARLY=1 only (A/B builds, with
+    // MI_SORT_LANE_BLOCKS=8: the second pass's registers spill at 16).
+#if MI_SORT_LANE_EARLY
     const bool early_wave = early_waves && (threadIdx.x >> 6) >= kBlock / 64 - early_waves;
     if (early_wave && S.small_base != 0xFFFFFFFFu) g_small = (n_full + S.small_base) / 8;
     for (int pass = 0; pass < 2; ++pass)
     {
     grab_limited = pass == 0 && early_wave;
+#else
+    (void)early_waves;
+    (void)early_rows;
+    {
+#endif
     uint32_t g_cur = grab();
     uint4 d_cur = load_desc(g_cur);
     uint32_t g_nxt = grab();
@@ -3088,6 +3101,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
+#if MI_SORT_LANE_EARLY
     if (pass == 0)
     {
         SORT_STAMP(5);
@@ -3096,6 +3110,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     }
     if (!early_wave) break;
     }  // pass
+#else
+    SORT_STAMP(5);
+    lane_items();
+    SORT_STAMP(6);
+    }
+#endif
     if (INLOOP) return;  // whole records were finished in the loop
     // Finish pass, in list order (round 5): a whole record's fold value W
     // (wr at its slot, eight consecutive words per group) is Z_m(raw) of its

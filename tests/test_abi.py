@@ -65,3 +65,27 @@ def test_no_device_fails_loudly():
     if "RAN" in out:
         pytest.skip("a GPU is present")
     assert "ERR -19" in out, out
+
+
+def test_cpu_flag_hashes_on_the_engine_cpu_path(oracle):
+    """MI_CRC32C_CPU (round 5): a host batch hashed on the engine's CPU path
+    by the caller's choice -- no device needed, counted in host_batches and
+    host_batch_bytes, never as a fallback; device pointers are refused."""
+    lib = E.lib()
+    rng = np.random.default_rng(21)
+    lengths = rng.integers(0, 3000, 500).astype(np.uint32)
+    offsets = np.zeros(500, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1].astype(np.uint64))
+    buf = rng.integers(0, 256, int(lengths.sum()) + 8, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, 500, dtype=np.uint32)
+    out = np.zeros(500, dtype=np.uint32)
+    before = E.stats()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    cpu = 0x10
+    assert lib.mi_crc32c_batch(p(buf), p(offsets), p(lengths), p(inits), 500, 0, p(out), cpu) == 0
+    assert np.array_equal(out, oracle.batch(buf, offsets, lengths, inits))
+    st = E.stats()
+    assert st["host_batches"] - before["host_batches"] == 1
+    assert st["host_batch_bytes"] - before["host_batch_bytes"] == int(lengths.sum())
+    assert st["fallback_calls"] == before["fallback_calls"]
+    assert lib.mi_crc32c_batch(p(buf), p(offsets), p(lengths), None, 500, 0, p(out), cpu | 0x1) != 0

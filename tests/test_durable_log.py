@@ -519,3 +519,33 @@ def test_append_crc_hook_writes_the_reference_frames(tmp_path, reference, oracle
     for recno, entry, crc, hdr_entry in frames:
         assert got[recno] == entry and crc == oracle.crc32c(0, hdr_entry)
     log.destroy()
+
+
+def test_flush_routing_rule_on_the_host(tmp_path, oracle):
+    """The routing rule without a GPU (CPU suite): with the default engine and
+    host_batch_max above every flush, each flush is checksummed on the CPU
+    route (host_flushes == flushes, counted in the engine's host_batches, no
+    fallback for them); the frames carry the reference CRCs."""
+    import consus_amd as E
+    saved = os.environ.pop("MI_DLOG_HOST_BATCH_MAX")
+    try:
+        log = DurableLog(1 << 16, host_batch_max=1 << 40)
+        d = tmp_path / "d"
+        assert log.open(str(d))
+        before = E.stats()
+        entries = [bytes([i % 256]) * (10 + (i * 31) % 700) for i in range(800)]
+        for i, e in enumerate(entries):
+            assert log.append(e) == i + 1
+        wait_durable(log, 800)
+        assert log.flushes() > 0 and log.host_flushes() == log.flushes()
+        st = E.stats()
+        assert st["host_batches"] - before["host_batches"] == log.flushes()
+        assert st["fallback_calls"] == before["fallback_calls"]
+        log.close()
+        frames = parse_frames(d / "file_a") + parse_frames(d / "file_b")
+        assert len(frames) == 800
+        for recno, entry, crc, hdr_entry in frames:
+            assert entries[recno - 1] == entry and crc == oracle.crc32c(0, hdr_entry)
+        log.destroy()
+    finally:
+        os.environ["MI_DLOG_HOST_BATCH_MAX"] = saved
