@@ -123,7 +123,8 @@ class Stats(C.Structure):
                 ("last_multi_devices", C.c_int32 * MAX_DEVICES),
                 ("zero_copy_batches", C.c_uint64),
                 ("hint_overflows", C.c_uint64), ("host_batches", C.c_uint64),
-                ("host_batch_bytes", C.c_uint64), ("sorted_one_launch", C.c_uint64)]
+                ("host_batch_bytes", C.c_uint64), ("sorted_one_launch", C.c_uint64),
+                ("window_batches", C.c_uint64)]
 
 _lib = None
 

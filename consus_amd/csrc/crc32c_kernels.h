@@ -40,7 +40,9 @@ constexpr int kTabLane = kTabZNeg + 128 * 1024; // Z_16, Z_12, Z_8, Z_4, Z_32, Z
                                                  // 64-entry tables each: [op][c][i] = Z(i << 6c)
                                                  // (lane fold; Z_128: the LDS-free row update)
 constexpr int kLaneOps = 7;
-constexpr int kTabWords = kTabLane + kLaneOps * 6 * 64;
+constexpr int kTabZWin = kTabLane + kLaneOps * 6 * 64;  // G^{2048 k}, k = 1..63 (window path)
+constexpr uint32_t kWinShifts = 64;
+constexpr int kTabWords = kTabZWin + (kWinShifts - 1) * 1024;
 
 // LDS image of the record kernels (bytes).
 constexpr uint32_t kLdsMain = 0;            // 128 KiB bank-private G^{128}
@@ -160,6 +162,19 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
                          const uint32_t* inits, uint64_t count, const SortedWorkspace& ws,
                          uint32_t* out, const uint32_t* tables, const uint32_t* pow2, int grid,
                          hipStream_t stream);
+
+// Window path (launch_window): mid-size batches of at most kWinMaxCount
+// records in one launch; each record cut into windows of kWinRows rows from
+// its end, one per team.  acc / cnt: count words each, zero before and after.
+constexpr uint32_t kWinRows = 16;
+constexpr uint32_t kWinBlock = 256;
+constexpr uint32_t kWinMaxCount = 4096;
+size_t window_lds_bytes(uint32_t count);
+uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap);
+hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
+                         uint32_t* acc, uint32_t* cnt, const uint32_t* tables, const uint32_t* pow2,
+                         int grid_cap, hipStream_t stream);
 
 hipError_t launch_chain(const uint32_t* crcs, const uint64_t* after, uint32_t np, uint32_t* out,
                         const uint32_t* pow2_tables, hipStream_t stream);

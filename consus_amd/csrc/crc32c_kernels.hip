@@ -3204,6 +3204,214 @@ uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, in
     return count + uint64_t(grid) * sorted_full_per_wg(count, total_bytes, plog, grid);
 }
 
+// ---------------------------------------------------------------------------
+// Window path (round 5, VERDICT r4 Next 4): mid-size device batches in ONE
+// launch, no cost kernel, no LDS table image.  A record [a, E) covers the
+// 128-B rows [Rs, Re); it is cut into windows of kWinRows rows counted back
+// from its end: window k = rows [Re - 16 (k + 1), Re - 16 k) within [Rs, Re).
+// A team (8 lanes) hashes one window: its 16 rows are issued at once (16
+// dwordx4 per lane in flight), folded through the lane tables (ds_bpermute,
+// 42 VGPRs loaded from L2 beside the descriptors -- the sorted kernel's
+// 152 KiB LDS image took 3.7 us to stage on a 1 MiB batch), and the team's
+// fold value W, the raw state of the window's bytes as of Re - 16 k, is moved
+// to the record's end and past the m = 128 Re - E masked bytes: Z_{2048 k - m}
+// (W), one L2 table for Z_{-m} and one for Z_{2048 k}.  ~init rides in the
+// record's first four bytes (the sorted kernel's init word; a record of < 4
+// bytes takes the seed Z_L(~init) instead).  The CRC is ~ the XOR of the
+// record's window values: a one-window record's team stores it; otherwise
+// every team XORs its value into acc[r] and counts itself in cnt[r], and the
+// last to count swaps acc[r] for 0, stores the CRC and resets cnt[r] (agent
+// scope, acq_rel on the count), so both stay zero between launches.
+// Tasks (r, window) are numbered by a prefix over the records that every
+// workgroup computes for itself in LDS (count <= kWinMaxCount): a handful of
+// L2 round trips instead of a second launch or a grid barrier.  A grid
+// smaller than the task count (understated total) loops; it never fails.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_min32(uint32_t x)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) x = min(x, uint32_t(__shfl_xor(int(x), d)));
+    return x;
+}
+
+__global__ __launch_bounds__(kWinBlock) void crc32c_window_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint32_t count,
+    uint32_t* __restrict__ out, uint32_t* __restrict__ acc, uint32_t* __restrict__ cnt,
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2)
+{
+    // LDS: a[count] (u64), first task[count], len[count], wave sums
+    uint64_t* const s_addr = reinterpret_cast<uint64_t*>(smem);
+    uint32_t* const s_pre = reinterpret_cast<uint32_t*>(smem + size_t(count) * 8);
+    uint32_t* const s_len = s_pre + count;
+    uint32_t* const s_wsum = s_len + count;
+    LaneTabs lt;
+    load_lane_tabs<6 * kLaneOps>(lt, tables);
+    // (1) windows per record (an empty record: one task, which stores init)
+    for (uint32_t i = threadIdx.x; i < count; i += kWinBlock)
+    {
+        const uint64_t a = uint64_t(base) + off[i];
+        const uint32_t L = len[i];
+        s_addr[i] = a;
+        s_len[i] = L;
+        const uint32_t rows = uint32_t(((a + L + kRowBytes - 1) >> 7) - (a >> 7));
+        s_pre[i] = L ? (rows + kWinRows - 1) / kWinRows : 1u;
+    }
+    __syncthreads();
+    // (2) exclusive prefix: a contiguous run of records per thread
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t per = (count + kWinBlock - 1) / kWinBlock;
+    const uint32_t i0 = min(count, threadIdx.x * per), i1 = min(count, i0 + per);
+    uint32_t own = 0;
+    for (uint32_t i = i0; i < i1; ++i) own += s_pre[i];
+    uint32_t x = own;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        const uint32_t y = uint32_t(__shfl_up(int(x), d));
+        if (lane >= uint32_t(d)) x += y;
+    }
+    if (lane == 63) s_wsum[wave] = x;
+    __syncthreads();
+    uint32_t run = x - own, ntask = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kWinBlock / 64; ++w)
+    {
+        const uint32_t s = s_wsum[w];
+        run += w < wave ? s : 0u;
+        ntask += s;
+    }
+    for (uint32_t i = i0; i < i1; ++i)
+    {
+        const uint32_t c = s_pre[i];
+        s_pre[i] = run;
+        run += c;
+    }
+    __syncthreads();
+
+    // (3) one window per team per round; the round loop is wave-uniform (the
+    // lane-table permutes need every lane of the wave)
+    const uint32_t tl = threadIdx.x & (kTeam - 1);
+    const uint32_t team = threadIdx.x / kTeam;
+    constexpr uint32_t kTeamsPerWg = kWinBlock / kTeam;
+    const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
+    for (uint32_t t0 = blockIdx.x * kTeamsPerWg; t0 + wave * 8 < ntask; t0 += gridDim.x * kTeamsPerWg)
+    {
+        const uint32_t t = t0 + team;
+        const bool live = t < ntask;
+        // the record: the last r with pre[r] <= t (pre[0] = 0)
+        uint32_t lo = 0, hi = count - 1;
+        while (live && lo < hi)
+        {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= t)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        const uint32_t r = lo;
+        const uint64_t a = s_addr[r];
+        const uint32_t L = live ? s_len[r] : 0u;
+        const uint32_t p0 = s_pre[r];
+        const uint32_t K = (r + 1 < count ? s_pre[r + 1] : ntask) - p0;
+        const uint32_t k = K - 1 - (t - p0);  // windows from the record's end
+        const uint32_t ninit = inits ? ~inits[r] : 0xFFFFFFFFu;
+        const uint64_t E = a + L;
+        const int64_t Rs = int64_t(a >> 7), Re = int64_t((E + kRowBytes - 1) >> 7);
+        const int64_t row0 = Re - int64_t(kWinRows) * (int64_t(k) + 1);  // window row 0
+        // first row of this team's bytes in the window; the wave folds from
+        // its teams' smallest
+        const uint32_t ist = L ? uint32_t(min(max(Rs - row0, int64_t(0)), int64_t(kWinRows))) : kWinRows;
+        const uint32_t imin = wave_min32(ist);
+        uint4 w[kWinRows];
+#pragma unroll
+        for (int i = 0; i < int(kWinRows); ++i)
+        {
+            const bool in = uint32_t(i) >= ist;
+            const uint64_t p = uint64_t(row0 + i) * kRowBytes + tl * 16u;
+            w[i] = make_uint4(0, 0, 0, 0);
+            if (uint32_t(i) >= imin)  // wave-uniform
+                w[i] = load16_edge(in ? reinterpret_cast<const uint8_t*>(p) : zero16);
+        }
+        // edges: bytes before a in row Rs, the init word (rows Rs, Rs + 1),
+        // bytes from E on in row Re - 1
+        const int64_t lb = int64_t(a) - (Rs * kRowBytes + int64_t(tl) * 16);  // a within this lane's block of row Rs
+        const int32_t f0 = int32_t(min(max(lb, int64_t(0)), int64_t(16)));
+        const int32_t be = int32_t(min(max(int64_t(E) - ((Re - 1) * kRowBytes + int64_t(tl) * 16), int64_t(0)), int64_t(16)));
+        const bool with_init = L >= 4;
+        uint32_t V[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < int(kWinRows); ++i)
+        {
+            if (uint32_t(i) < imin) continue;  // wave-uniform
+            uint4 d = w[i];
+            const int64_t row = row0 + i;
+            if (row == Rs) d = mask_from(d, f0);
+            if (with_init && (row == Rs || row == Rs + 1))
+            {
+                const int32_t q = int32_t(lb - (row - Rs) * kRowBytes);
+                d.x ^= init_dword(ninit, q, 0);
+                d.y ^= init_dword(ninit, q, 1);
+                d.z ^= init_dword(ninit, q, 2);
+                d.w ^= init_dword(ninit, q, 3);
+            }
+            if (row == Re - 1) d = mask_below(d, be);
+            row_update_lane(V, d, lt, true, false);
+        }
+        const uint32_t W = team_fold_lane(V, lt);
+        if (tl == 0 && live)
+        {
+            if (L == 0)
+                out[r] = ~ninit;  // crc32c(init, "", 0) = init
+            else
+            {
+                const uint32_t m = uint32_t(uint64_t(Re) * kRowBytes - E);
+                uint32_t v = zglob(tables + kTabZNeg + m * 1024u, W);
+                if (k) v = k < kWinShifts ? zglob(tables + kTabZWin + (k - 1) * 1024u, v)
+                                      : zshift48(pow2, v, uint64_t(k) * kWinRows * kRowBytes);
+                if (!with_init) v ^= zbits(tables + kTabP2, ninit, L);  // seed Z_L(~init)
+                if (K == 1)
+                    out[r] = ~v;
+                else
+                {
+                    __hip_atomic_fetch_xor(acc + r, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t seen = __hip_atomic_fetch_add(cnt + r, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                    if (seen == K - 1)
+                    {
+                        const uint32_t all = __hip_atomic_exchange(acc + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(cnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        out[r] = ~all;
+                    }
+                }
+            }
+        }
+    }
+}
+
+size_t window_lds_bytes(uint32_t count) { return size_t(count) * 16 + 16 * (kWinBlock / 64); }
+
+uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap)
+{
+    // windows <= L / 2048 + 1.125 per record (rows <= L / 128 + 2)
+    const uint64_t bound = total_bytes / (kWinRows * kRowBytes) + (9 * count) / 8 + 1;
+    const uint64_t g = (bound + kWinBlock / kTeam - 1) / (kWinBlock / kTeam);
+    return std::max<uint64_t>(1, std::min<uint64_t>(g, uint64_t(grid_cap)));
+}
+
+hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
+                         uint32_t* acc, uint32_t* cnt, const uint32_t* tables, const uint32_t* pow2,
+                         int grid_cap, hipStream_t stream)
+{
+    if (count == 0) return hipSuccess;
+    if (count > kWinMaxCount) return hipErrorInvalidValue;
+    const uint32_t g = uint32_t(window_grid(count, total_bytes, grid_cap));
+    hipLaunchKernelGGL(crc32c_window_kernel, dim3(g), dim3(kWinBlock), window_lds_bytes(uint32_t(count)),
+                       stream, static_cast<const uint8_t*>(base), offsets, lengths, inits,
+                       uint32_t(count), out, acc, cnt, tables, pow2);
+    return hipGetLastError();
+}
+
 // Allow the 152 KiB dynamic LDS image on the two persistent kernels.
 hipError_t configure_kernels()
 {
@@ -3229,6 +3437,10 @@ hipError_t configure_kernels()
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_window_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int(window_lds_bytes(kWinMaxCount)));
     const void* ks[] = {reinterpret_cast<const void*>(&crc32c_sorted_kernel<2>),
                         reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>)};
     for (const void* f : ks)

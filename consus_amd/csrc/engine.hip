@@ -155,6 +155,9 @@ int build_device(int device)
     for (int k = 1; k <= 32; ++k)
         make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZRows + (k - 1) * 1024]),
                          uint64_t(kRowBytes) * k);
+    for (uint32_t k = 1; k < kWinShifts; ++k)
+        make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZWin + (k - 1) * 1024]),
+                         uint64_t(kWinRows) * kRowBytes * k);
     {
         Op32 inv;
         if (!invert(zeros_op(kRowBytes), &inv))
@@ -331,6 +334,7 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
+    DevBuf win_acc;                        // window path: acc[count], cnt[count], kept zero
     DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
     uint32_t done_seq = 0;
     PinBuf pin_small;                   // plan-size read-back; word kDoneWord: completion word
@@ -422,7 +426,7 @@ struct Ctx
         sorted_users = nullptr;
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs, &srt_cost,
-                          &srt_ctrl, &srt_items, &done_ctr})
+                          &srt_ctrl, &srt_items, &win_acc, &done_ctr})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -574,7 +578,24 @@ int varpath_forced()
     const char* e = std::getenv("MI_CRC32C_VARPATH");
     if (e && !std::strcmp(e, "pieces")) return 1;
     if (e && !std::strcmp(e, "sorted")) return 2;
+    if (e && !std::strcmp(e, "window")) return 3;
     return 0;
+}
+
+// The window path (one launch, crc32c_kernels.hip "window path") takes device
+// batches of at most kWinMaxCount records and kWinMaxBytes bytes (total
+// given); MI_CRC32C_VARPATH=window forces it up to kWinMaxCount records,
+// =sorted / =pieces never.  MI_CRC32C_WIN_MAX_BYTES overrides the size bound
+// (probes; read per batch).
+constexpr uint64_t kWinMaxBytes = 16ull << 20;
+bool window_path(uint64_t count, uint64_t total_bytes)
+{
+    const int f = varpath_forced();
+    if (!total_bytes || count > kWinMaxCount || f == 1 || f == 2) return false;
+    if (f == 3) return true;
+    uint64_t cap = kWinMaxBytes;
+    if (const char* e = std::getenv("MI_CRC32C_WIN_MAX_BYTES")) cap = std::strtoull(e, nullptr, 10);
+    return total_bytes <= cap;
 }
 
 // A device buffer of at least `bytes` whose new allocations are zeroed (on the
@@ -713,6 +734,18 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     return MI_CRC32C_OK;
 }
 
+int run_window(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
+               const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
+{
+    int st;
+    if ((st = reserve_zeroed(c->win_acc, count * 8, c->stream))) return st;
+    uint32_t* acc = c->win_acc.as<uint32_t>();
+    HIP_TRY(launch_window(base, off, len, inits, count, total_bytes, out, acc, acc + count, d->d_tables,
+                          d->d_pow2, 8 * d->cus, c->stream));
+    mi_host::note_window_batch();
+    return MI_CRC32C_OK;
+}
+
 // MI_CRC32C_ZERO_COPY=0: host batches in mapped pinned memory are staged by
 // copy commands instead of read in place (A/B and tests; read per batch)
 bool zero_copy_disabled()
@@ -762,6 +795,8 @@ int run_var(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const
                               d->d_pow2, d->cus, c->stream, nullptr, direct_lite_mode()));
         return MI_CRC32C_OK;
     }
+    if (window_path(count, total_bytes))
+        return run_window(d, c, base, off, len, inits, count, total_bytes, out);
     if (total_bytes && count < kSortedMaxCount && varpath_forced() != 1)
         return run_sorted(d, c, base, off, len, inits, count, total_bytes, out);
     const uint32_t nb = var_plan_blocks(count);

@@ -69,7 +69,7 @@ bool have_sse42()
 
 std::atomic<uint64_t> g_gpu_calls{0}, g_fb_calls{0}, g_fb_bytes{0}, g_sharded{0}, g_sorted{0},
     g_routed_calls{0}, g_routed_bytes{0}, g_zero_copy{0}, g_hint_overflow{0},
-    g_host_batches{0}, g_host_batch_bytes{0}, g_sorted_one{0};
+    g_host_batches{0}, g_host_batch_bytes{0}, g_sorted_one{0}, g_window{0};
 std::atomic<int> g_fb_status{0};
 std::atomic<int> g_multi_ranges{0};
 std::atomic<int> g_multi_devs[MI_CRC32C_MAX_DEVICES];
@@ -116,6 +116,7 @@ void note_sorted_batch(bool one_launch)
     g_sorted.fetch_add(1, std::memory_order_relaxed);
     if (one_launch) g_sorted_one.fetch_add(1, std::memory_order_relaxed);
 }
+void note_window_batch() { g_window.fetch_add(1, std::memory_order_relaxed); }
 void note_zero_copy_batch() { g_zero_copy.fetch_add(1, std::memory_order_relaxed); }
 void note_hint_overflow() { g_hint_overflow.fetch_add(1, std::memory_order_relaxed); }
 void note_host_batch(uint64_t bytes)
@@ -154,6 +155,7 @@ void mi_crc32c_stats(mi_crc32c_stats_t* out)
     out->host_batches = mi_host::g_host_batches.load();
     out->host_batch_bytes = mi_host::g_host_batch_bytes.load();
     out->sorted_one_launch = mi_host::g_sorted_one.load();
+    out->window_batches = mi_host::g_window.load();
     out->last_fallback_status = mi_host::g_fb_status.load();
     const int ranges = mi_host::g_multi_ranges.load();
     out->last_multi_ranges = ranges;
@@ -173,6 +175,7 @@ void mi_crc32c_stats_reset(void)
     mi_host::g_host_batches.store(0);
     mi_host::g_host_batch_bytes.store(0);
     mi_host::g_sorted_one.store(0);
+    mi_host::g_window.store(0);
     mi_host::g_routed_calls.store(0);
     mi_host::g_routed_bytes.store(0);
     mi_host::g_fb_status.store(0);

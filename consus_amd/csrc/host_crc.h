@@ -31,6 +31,7 @@ void note_fallback(int status, uint64_t bytes);
 void note_gpu_call();
 void note_sharded_call();
 void note_sorted_batch(bool one_launch = false);
+void note_window_batch();
 void note_zero_copy_batch();
 void note_hint_overflow();
 void note_host_batch(uint64_t bytes);

@@ -104,6 +104,8 @@ typedef struct mi_crc32c_stats_t
                                      crossover) */
     uint64_t host_batch_bytes;    /* bytes of those batches */
     uint64_t sorted_one_launch;   /* sorted batches hashed in one launch (grid barrier) */
+    uint64_t window_batches;      /* variable-length batches hashed by the window path
+                                     (mid-size device batches, one launch) */
 } mi_crc32c_stats_t;
 void mi_crc32c_stats(mi_crc32c_stats_t* out);
 void mi_crc32c_stats_reset(void);

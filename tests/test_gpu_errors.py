@@ -131,9 +131,10 @@ def test_understated_size_hint_is_recovered(engine, oracle):
     d_off.upload(offsets)
     d_len.upload(lengths)
     want = oracle.batch(buf, offsets, lengths)
-    # a 4 KiB hint on the piece path; a 4 MiB hint (room for 129 descriptors)
-    # on the sorted path, whose split records need 64 + 960 of them
-    for hint, path in ((4096, None), (4 << 20, "sorted")):
+    # a 4 KiB hint on the piece path and on the window path (which sizes its
+    # grid from it and loops); a 4 MiB hint (room for 129 descriptors) on the
+    # sorted path, whose split records need 64 + 960 of them
+    for hint, path in ((4096, "pieces"), (4096, "window"), (4 << 20, "sorted")):
         d_out.upload(np.full(count, 0xABABABAB, dtype=np.uint32))
         errors = []
 

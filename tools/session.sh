@@ -19,6 +19,10 @@ while [ $# -gt 0 ]; do
   step=$1; shift
   case $step in
     tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    window) run pytest_window 300 python -u -m pytest tests/test_gpu_window.py tests/test_gpu_errors.py -x -q --timeout 120 --timeout-method thread &&
+            for rnd in 1 2; do for pth in window sorted; do
+              run mid_${pth}_$rnd 200 python3 tools/mid_probe.py --path $pth --mib ${WIN_MIB:-1,2,4,8,16} --reps 300
+            done; done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
     flush) run flush_probe 300 ./tools/flush_probe 1000 ;;
