@@ -36,12 +36,14 @@ constexpr int kTabZero = kTabZInv128 + 1024;    // 4 zero words (init 0 when ini
 constexpr int kTabFInit = kTabZero + 4;         // Z_n(0xFFFFFFFF), n = 0..4096 (init 0 seeds)
 constexpr int kTabZRows = kTabFInit + 4100;     // G^{128 k}, k = 1..32 (last-piece shifts)
 constexpr int kTabZNeg = kTabZRows + 32 * 1024; // Z_{-m} = (Z_m)^{-1}, m = 0..127 (direct kernel)
-constexpr int kTabLane = kTabZNeg + 128 * 1024; // Z_16, Z_12, Z_8, Z_4, Z_32, Z_64, Z_128 as six
-                                                 // 64-entry tables each: [op][c][i] = Z(i << 6c)
-                                                 // (lane fold; Z_128: the LDS-free row update)
-constexpr int kLaneOps = 7;
-constexpr int kTabZWin = kTabLane + kLaneOps * 6 * 64;  // G^{2048 k}, k = 1..63 (window path)
-constexpr uint32_t kWinShifts = 64;
+constexpr int kTabLane = kTabZNeg + 128 * 1024; // Z_16, Z_12, Z_8, Z_4, Z_32, Z_64, Z_128, Z_512,
+                                                 // Z_1024 as six 64-entry tables each:
+                                                 // [op][c][i] = Z(i << 6c) (lane fold; Z_128: the
+                                                 // LDS-free row update; Z_512, Z_1024: the window
+                                                 // path's chain joins)
+constexpr int kLaneOps = 9;
+constexpr int kTabZWin = kTabLane + kLaneOps * 6 * 64;  // G^{512 k}, k = 1..255 (window path)
+constexpr uint32_t kWinShifts = 256;
 constexpr int kTabWords = kTabZWin + (kWinShifts - 1) * 1024;
 
 // LDS image of the record kernels (bytes).
@@ -164,17 +166,21 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
                          hipStream_t stream);
 
 // Window path (launch_window): mid-size batches of at most kWinMaxCount
-// records in one launch; each record cut into windows of kWinRows rows from
-// its end, one per team.  acc / cnt: count words each, zero before and after.
-constexpr uint32_t kWinRows = 16;
-constexpr uint32_t kWinBlock = 256;
+// records in one launch; each record cut into windows of 4, 8 or 16 rows from
+// its end, one per team.  acc64 / acc / cnt: count words each, zero before
+// and after.
+constexpr uint32_t kWinBlockMax = 256;   // workgroup of batches above kWinSmallCount records
+constexpr uint32_t kWinSmallCount = 768;  // ... and one wave per workgroup up to it
 constexpr uint32_t kWinMaxCount = 4096;
 size_t window_lds_bytes(uint32_t count);
-uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap);
+uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_t block, uint32_t rows);
 hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
-                         uint32_t* acc, uint32_t* cnt, const uint32_t* tables, const uint32_t* pow2,
-                         int grid_cap, hipStream_t stream);
+                         uint64_t* acc64, uint32_t* acc, uint32_t* cnt, const uint32_t* tables,
+                         const uint32_t* pow2, int grid_cap,
+                         uint32_t block,  // 0: by count; 64, 256
+                         uint32_t rows,   // rows per window, 0: by size; 4, 8, 16
+                         hipStream_t stream);
 
 hipError_t launch_chain(const uint32_t* crcs, const uint64_t* after, uint32_t np, uint32_t* out,
                         const uint32_t* pow2_tables, hipStream_t stream);

@@ -1422,7 +1422,7 @@ __global__ __launch_bounds__(LITE ? kLiteBlock : kBlock, 1) void crc32c_direct_k
     }
     LaneTabs lt;
     if constexpr (LITE)
-        load_lane_tabs<6 * kLaneOps>(lt, tables);
+        load_lane_tabs<42>(lt, tables);  // the fold operators and Z_128
     else
         stage_tables(tables);
     for (uint64_t it = 0; it < iters; ++it)
@@ -3208,25 +3208,34 @@ uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, in
 // Window path (round 5, VERDICT r4 Next 4): mid-size device batches in ONE
 // launch, no cost kernel, no LDS table image.  A record [a, E) covers the
 // 128-B rows [Rs, Re); it is cut into windows of kWinRows rows counted back
-// from its end: window k = rows [Re - 16 (k + 1), Re - 16 k) within [Rs, Re).
-// A team (8 lanes) hashes one window: its 16 rows are issued at once (16
-// dwordx4 per lane in flight), folded through the lane tables (ds_bpermute,
-// 42 VGPRs loaded from L2 beside the descriptors -- the sorted kernel's
-// 152 KiB LDS image took 3.7 us to stage on a 1 MiB batch), and the team's
-// fold value W, the raw state of the window's bytes as of Re - 16 k, is moved
-// to the record's end and past the m = 128 Re - E masked bytes: Z_{2048 k - m}
-// (W), one L2 table for Z_{-m} and one for Z_{2048 k}.  ~init rides in the
-// record's first four bytes (the sorted kernel's init word; a record of < 4
-// bytes takes the seed Z_L(~init) instead).  The CRC is ~ the XOR of the
-// record's window values: a one-window record's team stores it; otherwise
-// every team XORs its value into acc[r] and counts itself in cnt[r], and the
-// last to count swaps acc[r] for 0, stores the CRC and resets cnt[r] (agent
-// scope, acq_rel on the count), so both stay zero between launches.
-// Tasks (r, window) are numbered by a prefix over the records that every
-// workgroup computes for itself in LDS (count <= kWinMaxCount): a handful of
-// L2 round trips instead of a second launch or a grid barrier.  A grid
-// smaller than the task count (understated total) loops; it never fails.
+// from its end: window k = rows [Re - 16 (k + 1), Re - 16 k) within [Rs, Re)
+// (K = ceil((L + 127) / 2048) windows: an upper bound taken from the length
+// alone, so the last may be empty).  A team (8 lanes) hashes one window: its
+// 16 rows are issued at once (16 dwordx4 per lane in flight) and folded
+// through the lane tables (ds_bpermute; the sorted kernel's 152 KiB LDS image
+// took 3.7 us to stage on a 1 MiB batch) as four independent chains of 4 rows,
+// joined with Z_512 and Z_1024 (a 16-row chain measured 3.8 us of a 1 MiB
+// batch's 13.1, profiles/r05_window_parts.txt).  The team's fold value W is the
+// raw state of the window's bytes as of row Re - 16 k; Z_{2048 k}(W) (one L2
+// table) moves it to row Re.  ~init rides in the record's first four bytes
+// (the sorted kernel's init word; a record of < 4 bytes takes the seed
+// Z_L(~init) instead).  The windows of a record that fall in one wave are
+// XORed there (team leaders' values through 16 permutes); a record within
+// one wave is finished by its first team: crc = ~Z_{-m}(XOR), m = 128 Re - E.
+// A record over several waves (segments) XORs each segment's value into the
+// low half of a 64-bit word acc[r] and its segment bit into the high half in
+// ONE atomic; the segment that completes the mask finishes the record and
+// zeroes the word (three dependent device-scope atomics per window measured
+// 1.8 / 4.8 / 17 us of a 1 / 4 / 16 MiB batch).  Records of more than 32
+// segments take the acc32 / cnt form (XOR, acq_rel count, swap).  All
+// workspace words are zero between launches.  Tasks (r, window) are numbered
+// by a prefix over the record lengths that every workgroup computes for
+// itself in LDS (count <= kWinMaxCount): no second launch, no grid barrier.
+// A grid smaller than the task count (understated total) loops; it never fails.
 // ---------------------------------------------------------------------------
+#ifndef MI_WIN_SKIP
+#define MI_WIN_SKIP 0  // A/B timing builds only (wrong CRCs): 1 no combine, 2 no lookups, 4 no fold
+#endif
 __device__ __forceinline__ uint32_t wave_min32(uint32_t x)
 {
 #pragma unroll
@@ -3234,33 +3243,33 @@ __device__ __forceinline__ uint32_t wave_min32(uint32_t x)
     return x;
 }
 
-__global__ __launch_bounds__(kWinBlock) void crc32c_window_kernel(
+template <uint32_t R>
+__device__ __forceinline__ uint32_t win_count(uint32_t L)
+{
+    return (L + kRowBytes - 1 + R * kRowBytes - 1) / (R * kRowBytes);
+}
+
+// B threads per workgroup, R rows per window (16, or 8 for batches that have
+// fewer windows than the chip has CUs: twice the waves, half the permutes each)
+template <uint32_t B, uint32_t R>
+__global__ __launch_bounds__(B) void crc32c_window_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint32_t count,
-    uint32_t* __restrict__ out, uint32_t* __restrict__ acc, uint32_t* __restrict__ cnt,
-    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2)
+    uint32_t* __restrict__ out, uint64_t* __restrict__ acc64, uint32_t* __restrict__ acc,
+    uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2)
 {
-    // LDS: a[count] (u64), first task[count], len[count], wave sums
-    uint64_t* const s_addr = reinterpret_cast<uint64_t*>(smem);
-    uint32_t* const s_pre = reinterpret_cast<uint32_t*>(smem + size_t(count) * 8);
-    uint32_t* const s_len = s_pre + count;
-    uint32_t* const s_wsum = s_len + count;
+    // LDS: first task of each record, wave sums
+    uint32_t* const s_pre = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* const s_wsum = s_pre + count;
     LaneTabs lt;
     load_lane_tabs<6 * kLaneOps>(lt, tables);
-    // (1) windows per record (an empty record: one task, which stores init)
-    for (uint32_t i = threadIdx.x; i < count; i += kWinBlock)
-    {
-        const uint64_t a = uint64_t(base) + off[i];
-        const uint32_t L = len[i];
-        s_addr[i] = a;
-        s_len[i] = L;
-        const uint32_t rows = uint32_t(((a + L + kRowBytes - 1) >> 7) - (a >> 7));
-        s_pre[i] = L ? (rows + kWinRows - 1) / kWinRows : 1u;
-    }
+    // (1) windows per record, from the lengths alone (an empty record: one
+    // task, which stores init)
+    for (uint32_t i = threadIdx.x; i < count; i += B) s_pre[i] = win_count<R>(len[i]);
     __syncthreads();
     // (2) exclusive prefix: a contiguous run of records per thread
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t per = (count + kWinBlock - 1) / kWinBlock;
+    const uint32_t per = (count + B - 1) / B;
     const uint32_t i0 = min(count, threadIdx.x * per), i1 = min(count, i0 + per);
     uint32_t own = 0;
     for (uint32_t i = i0; i < i1; ++i) own += s_pre[i];
@@ -3275,7 +3284,7 @@ __global__ __launch_bounds__(kWinBlock) void crc32c_window_kernel(
     __syncthreads();
     uint32_t run = x - own, ntask = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < kWinBlock / 64; ++w)
+    for (uint32_t w = 0; w < B / 64; ++w)
     {
         const uint32_t s = s_wsum[w];
         run += w < wave ? s : 0u;
@@ -3293,7 +3302,8 @@ __global__ __launch_bounds__(kWinBlock) void crc32c_window_kernel(
     // lane-table permutes need every lane of the wave)
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t team = threadIdx.x / kTeam;
-    constexpr uint32_t kTeamsPerWg = kWinBlock / kTeam;
+    const uint32_t tw = team & 7u;  // team within the wave
+    constexpr uint32_t kTeamsPerWg = B / kTeam;
     const uint8_t* zero16 = reinterpret_cast<const uint8_t*>(tables + kTabZero);
     for (uint32_t t0 = blockIdx.x * kTeamsPerWg; t0 + wave * 8 < ntask; t0 += gridDim.x * kTeamsPerWg)
     {
@@ -3310,22 +3320,22 @@ __global__ __launch_bounds__(kWinBlock) void crc32c_window_kernel(
                 hi = mid - 1;
         }
         const uint32_t r = lo;
-        const uint64_t a = s_addr[r];
-        const uint32_t L = live ? s_len[r] : 0u;
         const uint32_t p0 = s_pre[r];
         const uint32_t K = (r + 1 < count ? s_pre[r + 1] : ntask) - p0;
-        const uint32_t k = K - 1 - (t - p0);  // windows from the record's end
+        const uint32_t k = live ? K - 1 - (t - p0) : 0u;  // windows from the record's end
+        const uint64_t a = uint64_t(base) + off[r];
+        const uint32_t L = live ? len[r] : 0u;
         const uint32_t ninit = inits ? ~inits[r] : 0xFFFFFFFFu;
         const uint64_t E = a + L;
         const int64_t Rs = int64_t(a >> 7), Re = int64_t((E + kRowBytes - 1) >> 7);
-        const int64_t row0 = Re - int64_t(kWinRows) * (int64_t(k) + 1);  // window row 0
+        const int64_t row0 = Re - int64_t(R) * (int64_t(k) + 1);  // window row 0
         // first row of this team's bytes in the window; the wave folds from
         // its teams' smallest
-        const uint32_t ist = L ? uint32_t(min(max(Rs - row0, int64_t(0)), int64_t(kWinRows))) : kWinRows;
+        const uint32_t ist = L ? uint32_t(min(max(Rs - row0, int64_t(0)), int64_t(R))) : R;
         const uint32_t imin = wave_min32(ist);
-        uint4 w[kWinRows];
+        uint4 w[R];
 #pragma unroll
-        for (int i = 0; i < int(kWinRows); ++i)
+        for (int i = 0; i < int(R); ++i)
         {
             const bool in = uint32_t(i) >= ist;
             const uint64_t p = uint64_t(row0 + i) * kRowBytes + tl * 16u;
@@ -3339,9 +3349,10 @@ __global__ __launch_bounds__(kWinBlock) void crc32c_window_kernel(
         const int32_t f0 = int32_t(min(max(lb, int64_t(0)), int64_t(16)));
         const int32_t be = int32_t(min(max(int64_t(E) - ((Re - 1) * kRowBytes + int64_t(tl) * 16), int64_t(0)), int64_t(16)));
         const bool with_init = L >= 4;
-        uint32_t V[4] = {0, 0, 0, 0};
+        // chains of four rows
+        uint32_t V[R / 4][4] = {};
 #pragma unroll
-        for (int i = 0; i < int(kWinRows); ++i)
+        for (int i = 0; i < int(R); ++i)
         {
             if (uint32_t(i) < imin) continue;  // wave-uniform
             uint4 d = w[i];
@@ -3356,59 +3367,137 @@ __global__ __launch_bounds__(kWinBlock) void crc32c_window_kernel(
                 d.w ^= init_dword(ninit, q, 3);
             }
             if (row == Re - 1) d = mask_below(d, be);
-            row_update_lane(V, d, lt, true, false);
+            if (MI_WIN_SKIP & 4)
+            {
+                V[i >> 2][0] ^= d.x; V[i >> 2][1] ^= d.y; V[i >> 2][2] ^= d.z; V[i >> 2][3] ^= d.w;
+            }
+            else
+                row_update_lane(V[i >> 2], d, lt, true, false);
         }
-        const uint32_t W = team_fold_lane(V, lt);
-        if (tl == 0 && live)
+        uint32_t U[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
         {
+            if constexpr (R == 4)
+            {
+                U[q] = V[0][q];
+                continue;
+            }
+            const uint32_t lo8 = zL<7>(lt, V[0][q]) ^ V[1][q];  // Z_512: rows 0-7 as of row 7
+            if constexpr (R == 16)
+            {
+                const uint32_t hi8 = zL<7>(lt, V[2][q]) ^ V[3][q];  // rows 8-15 as of row 15
+                U[q] = zL<8>(lt, lo8) ^ hi8;                          // Z_1024
+            }
+            else
+                U[q] = lo8;
+        }
+        const uint32_t W = team_fold_lane(U, lt);
+        // this window's value as of row Re (team leaders; 0 for no record)
+        uint32_t T = live && L ? W : 0u;
+        if (k && !(MI_WIN_SKIP & 2))
+        {
+            const uint32_t kb = k * (R / 4);  // shift in 512 B
+            T = kb < kWinShifts ? zglob(tables + kTabZWin + (kb - 1) * 1024u, T)
+                                : zshift48(pow2, T, uint64_t(k) * R * kRowBytes);
+        }
+        // XOR over this wave's windows of the same record
+        const uint32_t rr = live ? r : 0xFFFFFFFFu;
+        uint32_t seg = 0;
+        bool lead = true;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+        {
+            const uint32_t rj = uint32_t(__shfl(int(rr), int(8 * j)));
+            const uint32_t Tj = uint32_t(__shfl(int(T), int(8 * j)));
+            seg ^= rj == rr ? Tj : 0u;
+            lead = lead && !(j < tw && rj == rr);
+        }
+        if (tl == 0 && live && lead)
+        {
+            bool fin = true;
             if (L == 0)
                 out[r] = ~ninit;  // crc32c(init, "", 0) = init
             else
             {
-                const uint32_t m = uint32_t(uint64_t(Re) * kRowBytes - E);
-                uint32_t v = zglob(tables + kTabZNeg + m * 1024u, W);
-                if (k) v = k < kWinShifts ? zglob(tables + kTabZWin + (k - 1) * 1024u, v)
-                                      : zshift48(pow2, v, uint64_t(k) * kWinRows * kRowBytes);
-                if (!with_init) v ^= zbits(tables + kTabP2, ninit, L);  // seed Z_L(~init)
-                if (K == 1)
-                    out[r] = ~v;
-                else
+                const uint32_t wf = p0 >> 3, wl = (p0 + K - 1) >> 3;  // the record's first and last waves
+                const uint32_t nseg = wl - wf + 1;
+                if (nseg > 1 && !(MI_WIN_SKIP & 1))
                 {
-                    __hip_atomic_fetch_xor(acc + r, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t seen = __hip_atomic_fetch_add(cnt + r, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-                    if (seen == K - 1)
+                    if (nseg <= 32)
                     {
-                        const uint32_t all = __hip_atomic_exchange(acc + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(cnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        out[r] = ~all;
+                        const uint32_t sb = 1u << ((t >> 3) - wf);
+                        const uint64_t old = __hip_atomic_fetch_xor(acc64 + r, (uint64_t(sb) << 32) | seg,
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t full = nseg == 32 ? 0xFFFFFFFFu : (1u << nseg) - 1u;
+                        fin = (uint32_t(old >> 32) | sb) == full;
+                        if (fin)
+                        {
+                            seg ^= uint32_t(old);
+                            __hip_atomic_store(acc64 + r, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
                     }
+                    else
+                    {
+                        __hip_atomic_fetch_xor(acc + r, seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t seen = __hip_atomic_fetch_add(cnt + r, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                        fin = seen == nseg - 1;
+                        if (fin)
+                        {
+                            seg = __hip_atomic_exchange(acc + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(cnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                }
+                if (fin)
+                {
+                    const uint32_t m = uint32_t(uint64_t(Re) * kRowBytes - E);
+                    uint32_t v = (MI_WIN_SKIP & 2) ? seg : zglob(tables + kTabZNeg + m * 1024u, seg);
+                    if (!with_init) v ^= zbits(tables + kTabP2, ninit, L);  // seed Z_L(~init)
+                    out[r] = ~v;
                 }
             }
         }
     }
 }
 
-size_t window_lds_bytes(uint32_t count) { return size_t(count) * 16 + 16 * (kWinBlock / 64); }
+size_t window_lds_bytes(uint32_t count) { return size_t(count) * 4 + 4 * (kWinBlockMax / 64); }
 
-uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap)
+uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_t block, uint32_t rows)
 {
-    // windows <= L / 2048 + 1.125 per record (rows <= L / 128 + 2)
-    const uint64_t bound = total_bytes / (kWinRows * kRowBytes) + (9 * count) / 8 + 1;
-    const uint64_t g = (bound + kWinBlock / kTeam - 1) / (kWinBlock / kTeam);
+    // windows <= L / 2048 + 1.07 per record (win_count)
+    const uint64_t bound = total_bytes / (rows * kRowBytes) + (17 * count) / 16 + 1;
+    const uint64_t g = (bound + block / kTeam - 1) / (block / kTeam);
     return std::max<uint64_t>(1, std::min<uint64_t>(g, uint64_t(grid_cap)));
 }
 
 hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
-                         uint32_t* acc, uint32_t* cnt, const uint32_t* tables, const uint32_t* pow2,
-                         int grid_cap, hipStream_t stream)
+                         uint64_t* acc64, uint32_t* acc, uint32_t* cnt, const uint32_t* tables,
+                         const uint32_t* pow2, int grid_cap, uint32_t block, uint32_t rows,
+                         hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
     if (count > kWinMaxCount) return hipErrorInvalidValue;
-    const uint32_t g = uint32_t(window_grid(count, total_bytes, grid_cap));
-    hipLaunchKernelGGL(crc32c_window_kernel, dim3(g), dim3(kWinBlock), window_lds_bytes(uint32_t(count)),
-                       stream, static_cast<const uint8_t*>(base), offsets, lengths, inits,
-                       uint32_t(count), out, acc, cnt, tables, pow2);
+    // one-wave workgroups spread a small batch's lane-table permutes over as
+    // many CUs as it has waves; 4-wave ones read the lengths fewer times
+    if (block == 0) block = count <= kWinSmallCount ? 64u : kWinBlockMax;
+    // 4-row windows up to 12 waves of them per CU (grid_cap / 8 = the CUs),
+    // then 8: configs[2] records cut to 1 / 2 / 4 / 8 / 16 MiB took 7.2 / 8.4
+    // / 9.3 / 12.6 / 21.5 us with 4 rows, 8.7 / 9.7 / 10.2 / 13.8 / 17.4 with 8,
+    // 12.0 / 12.8 / 13.8 / 15.0 / 20.3 with 16 (profiles/r05_window_rows.txt)
+    if (rows == 0)
+        rows = window_grid(count, total_bytes, 1 << 30, 64, 4) <= 12 * (uint64_t(grid_cap) / 8) ? 4u : 8u;
+    const uint32_t g = uint32_t(window_grid(count, total_bytes, grid_cap, block, rows));
+    auto k = block == 64 ? (rows == 4   ? crc32c_window_kernel<64, 4>
+                            : rows == 8 ? crc32c_window_kernel<64, 8>
+                                        : crc32c_window_kernel<64, 16>)
+                         : (rows == 4   ? crc32c_window_kernel<kWinBlockMax, 4>
+                            : rows == 8 ? crc32c_window_kernel<kWinBlockMax, 8>
+                                        : crc32c_window_kernel<kWinBlockMax, 16>);
+    hipLaunchKernelGGL(k, dim3(g), dim3(block), window_lds_bytes(uint32_t(count)), stream,
+                       static_cast<const uint8_t*>(base), offsets, lengths, inits, uint32_t(count),
+                       out, acc64, acc, cnt, tables, pow2);
     return hipGetLastError();
 }
 
@@ -3437,10 +3526,16 @@ hipError_t configure_kernels()
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&single_join_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSingleStaged * 4096);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_window_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                int(window_lds_bytes(kWinMaxCount)));
+    const void* kw[] = {reinterpret_cast<const void*>(&crc32c_window_kernel<64, 4>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockMax, 4>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<64, 8>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<64, 16>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockMax, 8>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockMax, 16>)};
+    for (const void* f : kw)
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    int(window_lds_bytes(kWinMaxCount)));
     const void* ks[] = {reinterpret_cast<const void*>(&crc32c_sorted_kernel<2>),
                         reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>)};
     for (const void* f : ks)

@@ -157,7 +157,7 @@ int build_device(int device)
                          uint64_t(kRowBytes) * k);
     for (uint32_t k = 1; k < kWinShifts; ++k)
         make_fold_tables(reinterpret_cast<uint32_t(*)[256]>(&img[kTabZWin + (k - 1) * 1024]),
-                         uint64_t(kWinRows) * kRowBytes * k);
+                         uint64_t(512) * k);
     {
         Op32 inv;
         if (!invert(zeros_op(kRowBytes), &inv))
@@ -173,7 +173,7 @@ int build_device(int device)
     }
     {
         // lane-fold tables: 6-bit slices of the team fold's six shifts (chunk 5 holds bits 30-31)
-        const uint64_t shifts[kLaneOps] = {16, 12, 8, 4, 32, 64, kRowBytes};
+        const uint64_t shifts[kLaneOps] = {16, 12, 8, 4, 32, 64, kRowBytes, 512, 1024};
         for (int k = 0; k < kLaneOps; ++k)
         {
             const Op32 z = zeros_op(shifts[k]);
@@ -334,7 +334,7 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
-    DevBuf win_acc;                        // window path: acc[count], cnt[count], kept zero
+    DevBuf win_acc;                        // window path: acc64[count], acc[count], cnt[count], kept zero
     DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
     uint32_t done_seq = 0;
     PinBuf pin_small;                   // plan-size read-back; word kDoneWord: completion word
@@ -738,10 +738,17 @@ int run_window(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
 {
     int st;
-    if ((st = reserve_zeroed(c->win_acc, count * 8, c->stream))) return st;
-    uint32_t* acc = c->win_acc.as<uint32_t>();
-    HIP_TRY(launch_window(base, off, len, inits, count, total_bytes, out, acc, acc + count, d->d_tables,
-                          d->d_pow2, 8 * d->cus, c->stream));
+    if ((st = reserve_zeroed(c->win_acc, count * 16, c->stream))) return st;
+    uint64_t* acc64 = c->win_acc.as<uint64_t>();
+    uint32_t* acc = reinterpret_cast<uint32_t*>(acc64 + count);
+    // MI_CRC32C_WIN_BLOCK=64|256, MI_CRC32C_WIN_ROWS=4|8|16: the workgroup and
+    // the window (A/B, tests; default by count and size)
+    uint32_t block = 0, rows = 0;
+    if (const char* e = std::getenv("MI_CRC32C_WIN_BLOCK")) block = std::atoi(e) == 64 ? 64u : 256u;
+    if (const char* e = std::getenv("MI_CRC32C_WIN_ROWS"))
+        rows = std::atoi(e) == 4 ? 4u : std::atoi(e) == 8 ? 8u : 16u;
+    HIP_TRY(launch_window(base, off, len, inits, count, total_bytes, out, acc64, acc, acc + count,
+                          d->d_tables, d->d_pow2, 8 * d->cus, block, rows, c->stream));
     mi_host::note_window_batch();
     return MI_CRC32C_OK;
 }

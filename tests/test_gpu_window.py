@@ -1,12 +1,16 @@
 """GPU parity of the window path (crc32c_kernels.hip "window path", DESIGN.md
 section 4.8): mid-size device batches (at most kWinMaxCount = 4096 records,
 16 MiB by default) in one launch.  Each record is cut into windows of 16
-rows (2 KiB) counted back from its end, one window per team; a record of
+rows (2 KiB; 8 rows while the batch has fewer waves of them than the chip
+has CUs) counted back from its end, one window per team; a record of
 several windows is combined through acc[] / cnt[] (XOR and count, the last
 team stores the CRC and zeroes both).  Every result is compared with the
 CPU oracle, bit-exact; the path is checked to have run
 (mi_crc32c_stats().window_batches).  MI_CRC32C_VARPATH=window forces the path
-up to 4096 records; without it, the engine takes it by size.
+up to 4096 records; without it, the engine takes it by size.  Each forced
+test runs with the workgroup and window the engine picks by count and size,
+and with one-wave / four-wave workgroups (MI_CRC32C_WIN_BLOCK) and 8 / 16-row
+windows (MI_CRC32C_WIN_ROWS, also 4) forced.
 """
 import os
 
@@ -16,12 +20,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def window_path(engine):
+@pytest.fixture(params=[{}, {"MI_CRC32C_WIN_BLOCK": "64"}, {"MI_CRC32C_WIN_BLOCK": "256"},
+                        {"MI_CRC32C_WIN_ROWS": "4"}, {"MI_CRC32C_WIN_ROWS": "8"},
+                        {"MI_CRC32C_WIN_ROWS": "16"}],
+                ids=["by_size", "block_64", "block_256", "rows_4", "rows_8", "rows_16"])
+def window_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "window"
+    os.environ.update(request.param)
     before = engine.stats()["window_batches"]
     yield lambda: engine.stats()["window_batches"] - before
+    for k in request.param:
+        os.environ.pop(k, None)
     if old is None:
         del os.environ["MI_CRC32C_VARPATH"]
     else:

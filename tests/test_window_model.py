@@ -3,7 +3,7 @@ kernel is tested against the oracle in tests/test_gpu_window.py).
 
 crc32c_kernels.hip, "window path": a record [a, E) covers the 128-B rows
 [Rs, Re); window k (k = 0 at the record's end) is rows
-[Re - 16 (k + 1), Re - 16 k).  A team's fold value W_k is the raw CRC (from a
+[Re - 16 (k + 1), Re - 16 k) (or 8-row windows, the same with 8).  A team's fold value W_k is the raw CRC (from a
 zero register) of the window's bytes with everything outside the record
 zeroed and ~init XORed over the record's first four bytes (records of >= 4
 bytes; shorter ones take the seed Z_L(~init)), evaluated at the window's last
@@ -16,7 +16,7 @@ spill.
 import numpy as np
 import pytest
 
-ROW, WIN = 128, 16
+ROW = 128
 
 
 def _raw0(oracle, data):
@@ -24,7 +24,7 @@ def _raw0(oracle, data):
     return (~oracle.crc32c(0xFFFFFFFF, data)) & 0xFFFFFFFF
 
 
-def _windows(oracle, buf, base, off, L, init):
+def _windows(oracle, buf, base, off, L, init, WIN):
     a = base + off
     E = a + L
     Rs, Re = a // ROW, (E + ROW - 1) // ROW
@@ -46,8 +46,8 @@ def _windows(oracle, buf, base, off, L, init):
     return acc, Re * ROW - E, K
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_window_decomposition_matches_the_oracle(oracle, seed):
+@pytest.mark.parametrize("seed,win", [(1, 16), (2, 16), (3, 8), (4, 4)])
+def test_window_decomposition_matches_the_oracle(oracle, seed, win):
     rng = np.random.default_rng(seed)
     base = 0x10000
     size = 1 << 18
@@ -62,7 +62,7 @@ def test_window_decomposition_matches_the_oracle(oracle, seed):
                 continue
             init = int(rng.integers(0, 2**32))
             crc = oracle.crc32c(init, buf[off:off + L])
-            acc, m, K = _windows(oracle, buf, base, off, L, init)
+            acc, m, K = _windows(oracle, buf, base, off, L, init, win)
             seen_k = max(seen_k, K)
             if L == 0:  # the kernel gives it one task, which stores init
                 continue

@@ -23,6 +23,18 @@ while [ $# -gt 0 ]; do
             for rnd in 1 2; do for pth in window sorted; do
               run mid_${pth}_$rnd 200 python3 tools/mid_probe.py --path $pth --mib ${WIN_MIB:-1,2,4,8,16} --reps 300
             done; done ;;
+    winblock) for rnd in 1 2; do for b in 64 256; do
+             MI_CRC32C_WIN_BLOCK=$b timeout -k 10 120 python3 tools/mid_probe.py --path window --mib ${WIN_MIB:-1,2,4,8,16} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd block=$b /"
+           done; done | tee "$OUT/winblock.out" ;;
+    winbig) for rnd in 1 2; do for cfg in "window 8 256" "window 16 256" "window 8 64" "sorted 0 0"; do
+             set -- $cfg; MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 /"
+           done; done | tee "$OUT/winbig.out" ;;
+    winrows) for rnd in 1 2; do for r in ${WIN_ROWS:-4 8 16}; do
+             MI_CRC32C_WIN_ROWS=$r timeout -k 10 120 python3 tools/mid_probe.py --path window --mib ${WIN_MIB:-1,2,4} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$r /"
+           done; done | tee "$OUT/winrows.out" ;;
+    wskip) for rnd in 1 2; do for v in ${WSKIP_LIBS:-w0 wskip1 wskip2 wskip4 wskip3 wskip7}; do
+             timeout -k 10 120 python3 tools/mid_probe.py --lib tools/ab/libconsus_crc32c_$v.so --path window --mib ${WIN_MIB:-1,4,16} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd /"
+           done; done | tee "$OUT/wskip.out" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
     flush) run flush_probe 300 ./tools/flush_probe 1000 ;;
