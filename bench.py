@@ -811,6 +811,55 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
     return res
 
 
+def run_mid(E, sizes_mib=(1, 4, 16, 64, 256), reps: int = 200) -> dict:
+    """Mid-size device batches (VERDICT r4 Next 4; a durable-log segment,
+    /root/reference/txman/durable_log.cc:287-347): configs[2]'s record stream
+    cut to N MiB, one batch per launch on the engine's own path choice (the
+    window path up to 16 MiB / 4096 records, the sorted path above), HIP
+    events over `reps` back-to-back batches after a warm-up; every size's
+    CRCs checked against the oracle (a checker, outside the timed region)."""
+    from consus_amd import workload as W
+    from oracle.oracle import Oracle
+    off_all, ln_all, _ = W.zipf_records(1 << 20)
+    cum = np.cumsum(ln_all, dtype=np.uint64)
+    top = int(np.searchsorted(cum, np.uint64(max(sizes_mib)) << np.uint64(20))) + 1
+    nbytes = int(cum[top - 1])
+    data = E.DeviceBuffer(nbytes + 16)
+    data.fill_splitmix64(W.DATA_SEED)
+    host = data.download(np.uint8, nbytes)
+    d_off, d_len, out = E.DeviceBuffer(top * 8), E.DeviceBuffer(top * 4), E.DeviceBuffer(top * 4)
+    O = Oracle()
+    rows = []
+    try:
+        for mib in sizes_mib:
+            n = int(np.searchsorted(cum, np.uint64(mib) << np.uint64(20))) + 1
+            off, ln = off_all[:n], ln_all[:n]
+            total = int(ln.sum(dtype=np.uint64))
+            d_off.upload(off)
+            d_len.upload(ln)
+            st0 = E.stats()
+            E.device_batch(data, d_off, d_len, n, out, total_bytes=total)
+            st1 = E.stats()
+            path = ("window" if st1["window_batches"] > st0["window_batches"] else
+                    "sorted" if st1["sorted_batches"] > st0["sorted_batches"] else "other")
+            ok = bool(np.array_equal(out.download(np.uint32, n), O.batch(host, off, ln)))
+            for _ in range(max(reps // 4, 20)):
+                E.device_batch(data, d_off, d_len, n, out, total_bytes=total, asynchronous=True)
+            E.sync()
+            E.timer_start()
+            for _ in range(reps):
+                E.device_batch(data, d_off, d_len, n, out, total_bytes=total, asynchronous=True)
+            ms = E.timer_stop() / reps
+            rows.append({"mib": mib, "records": n, "bytes": total, "us_per_batch": round(ms * 1e3, 2),
+                         "gb_s": round(total / (ms * 1e-3) / 1e9, 1), "path": path, "crc_ok": ok})
+    finally:
+        for b in (data, d_off, d_len, out):
+            b.free()
+    return {"unit": "us per device batch", "reps": reps,
+            "workload": "configs[2] records (Zipf 64 B - 64 KiB) cut to N MiB, device-resident",
+            "batches": rows}
+
+
 def run_single_split(args, E, dist, rank, world):
     """One record of world x 4 GiB, rank r holding bytes [4 GiB r, 4 GiB (r+1))
     of stream 0xC0DE in its HBM (a record split across GPUs).
@@ -1141,6 +1190,15 @@ def main():
             r = {"error": f"{type(e).__name__}: {e}"[:300]}
         r["leg_wall_s"] = round(time.perf_counter() - t_leg, 2)
         leg_res[key] = r
+    if legs:
+        t_leg = time.perf_counter()
+        try:
+            progress("leg mid_batches")
+            r = run_mid(E)
+        except Exception as e:  # noqa: BLE001
+            r = {"error": f"{type(e).__name__}: {e}"[:300]}
+        r["leg_wall_s"] = round(time.perf_counter() - t_leg, 2)
+        leg_res["mid_batches"] = r
 
     total_bytes = world * R * L * args.steps
     value = total_bytes / wall / 2**30
