@@ -586,8 +586,11 @@ int varpath_forced()
 // batches of at most kWinMaxCount records and kWinMaxBytes bytes (total
 // given); MI_CRC32C_VARPATH=window forces it up to kWinMaxCount records,
 // =sorted / =pieces never.  MI_CRC32C_WIN_MAX_BYTES overrides the size bound
-// (probes; read per batch).
-constexpr uint64_t kWinMaxBytes = 16ull << 20;
+// (probes; read per batch).  configs[2] records cut to 16 / 32 MiB (3811 /
+// 7481 records): 17.4 / 30.7 us against the sorted path's 25.3 / 27.5
+// (profiles/r05_window_vs_sorted_large.txt); the record bound (4096) ends the
+// window path first for such batches.
+constexpr uint64_t kWinMaxBytes = 24ull << 20;
 bool window_path(uint64_t count, uint64_t total_bytes)
 {
     const int f = varpath_forced();

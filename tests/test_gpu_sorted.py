@@ -299,9 +299,10 @@ def _device_run_no_hint(engine, buf, offsets, lengths):
 @pytest.mark.parametrize("mib", [1, 64, 300, 400])
 def test_sorted_default_with_known_total(engine, oracle, mib):
     """Without the knob, a device batch whose total is given takes the sorted
-    path at every size (round 4: with batch-sized pieces it is the faster
-    path from 1 MiB up); without the total, the piece path (its plan reads
-    the item count back)."""
+    path above 24 MiB or 4096 records (round 4: with batch-sized pieces it is
+    the faster path from 1 MiB up; round 5: below that bound the one-launch
+    window path, tests/test_gpu_window.py); without the total, the piece path
+    (its plan reads the item count back)."""
     rng = np.random.default_rng(19 + mib)
     count = (mib << 20) // 3400 + 1
     lengths = rng.integers(3300, 3500, count).astype(np.uint32)
@@ -309,9 +310,10 @@ def test_sorted_default_with_known_total(engine, oracle, mib):
     offsets, end = _packed(rng, lengths)
     buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
     want = oracle.batch(buf, offsets, lengths)
-    before = engine.stats()["sorted_batches"]
+    path = "window_batches" if end <= (24 << 20) and count <= 4096 else "sorted_batches"
+    before = engine.stats()[path]
     assert np.array_equal(_device_run(engine, buf, offsets, lengths), want)
-    assert engine.stats()["sorted_batches"] == before + 1
+    assert engine.stats()[path] == before + 1
     if mib <= 64:
         before = engine.stats()["sorted_batches"]
         assert np.array_equal(_device_run_no_hint(engine, buf, offsets, lengths), want)

@@ -1,6 +1,6 @@
 """GPU parity of the window path (crc32c_kernels.hip "window path", DESIGN.md
-section 4.8): mid-size device batches (at most kWinMaxCount = 4096 records,
-16 MiB by default) in one launch.  Each record is cut into windows of 16
+section 4.9): mid-size device batches (at most kWinMaxCount = 4096 records,
+24 MiB by default) in one launch.  Each record is cut into windows of 16
 rows (2 KiB; 8 rows while the batch has fewer waves of them than the chip
 has CUs) counted back from its end, one window per team; a record of
 several windows is combined through acc[] / cnt[] (XOR and count, the last
@@ -200,18 +200,18 @@ def test_window_empty_records_only(engine, oracle, window_path):
 
 
 def test_window_default_routing_by_size(engine, oracle):
-    """Without MI_CRC32C_VARPATH: a 1 MiB configs[2]-like batch (Zipf
-    64 B - 64 KiB) takes the window path, a 20 MiB one the sorted path."""
+    """Without MI_CRC32C_VARPATH: a 1 MiB and a 16 MiB configs[2]-like batch
+    (Zipf 64 B - 64 KiB) take the window path, one of 4200 records (20 MiB)
+    the sorted path."""
     assert "MI_CRC32C_VARPATH" not in os.environ
     rng = np.random.default_rng(13)
-    for count, path in ((230, "window_batches"), (4000, "sorted_batches")):
+    for count, path in ((230, "window_batches"), (3811, "window_batches"), (4200, "sorted_batches")):
         lengths = engine.zipf_lengths(0xDA7A5EED, count).astype(np.uint32)
         offsets, end = _packed(rng, lengths)
         buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
-        small = end <= (16 << 20)
         before = engine.stats()[path]
         _check(engine, oracle, buf, offsets, lengths)
-        assert engine.stats()[path] == before + 1, (count, end, small)
+        assert engine.stats()[path] == before + 1, (count, end)
 
 
 def test_window_host_batch_with_long_records(engine, oracle):
