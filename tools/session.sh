@@ -26,6 +26,17 @@ while [ $# -gt 0 ]; do
     winblock) for rnd in 1 2; do for b in 64 256; do
              MI_CRC32C_WIN_BLOCK=$b timeout -k 10 120 python3 tools/mid_probe.py --path window --mib ${WIN_MIB:-1,2,4,8,16} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd block=$b /"
            done; done | tee "$OUT/winblock.out" ;;
+    fetchsplit) C="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+             for cfg in fixed4k zipf; do
+               (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/fs_$cfg" -o k -- python3 "$ROOT/bench.py" --child-pmc --config $cfg --records-per-rank 1048576 --record-bytes 4096 > "$OUT/fs_$cfg.log" 2>&1) || { tail -5 "$OUT/fs_$cfg.log"; exit 1; }
+               echo "== $cfg"; python3 tools/pmc_summary.py "$OUT/fs_$cfg" crc32c_fixed_pipe crc32c_sorted_kernel sorted_cost_kernel
+             done | tee "$OUT/fetchsplit.out"
+             for m in keep drop; do
+               envs="ZIPF_WARM=2 ZIPF_ROUNDS=1 MI_CRC32C_SORT_PIECE_LOG2=16 MI_CRC32C_SORT_RING=2"; [ "$m" = keep ] && envs="$envs ZIPF_KEEP_BELOW=1024"; [ "$m" = drop ] && envs="$envs ZIPF_DROP_BELOW=1024"
+               (cd /tmp && env $envs timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/fs_$m" -o k -- python3 "$ROOT/tools/zipf_probe.py" > "$OUT/fs_$m.log" 2>&1) || { tail -5 "$OUT/fs_$m.log"; exit 1; }
+               echo "== $m"; python3 tools/pmc_summary.py "$OUT/fs_$m" crc32c_sorted_kernel sorted_cost_kernel
+             done | tee -a "$OUT/fetchsplit.out"
+             rm -rf "$OUT"/fs_*/ ;;
     midhead) run mid_head 300 python3 -u tools/mid_probe.py --mib ${MID_MIB:-1,2,4,8,16,32,64,256} --reps 300 ;;
     winbig) for rnd in 1 2; do for cfg in "window 8 256" "window 16 256" "window 8 64" "sorted 0 0"; do
              set -- $cfg; MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 /"
