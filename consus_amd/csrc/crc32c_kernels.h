@@ -145,9 +145,6 @@ struct SortedWorkspace
     // ctrl[32] counts arrivals, bar_base = its value before this launch.
     int fused;
     uint32_t bar_base;
-    // early_waves << 16 | early_rows: waves that take the lane items once the
-    // list reaches team items of <= early_rows rows (0: none)
-    uint32_t lane_early;
 };
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);

@@ -2040,7 +2040,6 @@ struct SortShared
     uint32_t next_group;
     uint32_t next_lane;        // lane items taken (64 per grab)
     uint32_t lane_base;        // the first lane item's position among the last pieces
-    uint32_t small_base;       // ... the first team item of <= early_rows rows
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
     uint32_t bar_ok;           // fused launch: the grid barrier completed
@@ -2444,9 +2443,6 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #ifndef MI_SORT_LANE_BLOCKS
 #define MI_SORT_LANE_BLOCKS 16
 #endif
-#ifndef MI_SORT_LANE_EARLY
-#define MI_SORT_LANE_EARLY 0
-#endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 #define SORT_STAMP(k)                                                                        \
@@ -2470,11 +2466,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
-    uint32_t lrows, int fused, uint32_t bar_base, uint32_t lane_early)
+    uint32_t lrows, int fused, uint32_t bar_base)
 {
-    // the last early_waves waves of the workgroup take the lane items as soon
-    // as the list reaches team items of <= early_rows rows (round 5, below)
-    const uint32_t early_waves = lane_early >> 16, early_rows = lane_early & 0xFFFFu;
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint64_t piece = uint64_t(1) << plog;
     const uint32_t rows_max = uint32_t(piece / kRowBytes) + 1;  // rows of a full piece, unaligned
@@ -2483,7 +2476,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     if (threadIdx.x == 0) S.next_lane = 0;
-    if (threadIdx.x == 0) S.small_base = 0xFFFFFFFFu;
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
     // whole records finished in the loop (RB = 4, small batches) or by the
@@ -2636,9 +2628,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const uint32_t e = uint32_t(block_excl_scan64(c, S.wsum, total));
         if (threadIdx.x < kSortBins) S.bins[threadIdx.x] = e;
         if (threadIdx.x == kSortRows - lrows) S.lane_base = e;  // lane items follow the team items
-#if MI_SORT_LANE_EARLY
-        if (early_waves && threadIdx.x == kSortRows - early_rows) S.small_base = e;
-#endif
         if (threadIdx.x == 0)
         {
             // full pieces go to this workgroup's own region of fpw slots
@@ -2740,19 +2729,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
-    // (round 5) a wave that takes the lane items early stops taking groups
-    // once the next one is a group of small team items (g_small)
-    bool grab_limited = false;
-    uint32_t g_small = 0xFFFFFFFFu;
     auto grab = [&]() {
         uint32_t g = 0;
-        if (lane == 0)
-        {
-            if (grab_limited && __hip_atomic_load(&S.next_group, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= g_small)
-                g = 0xFFFFFFFFu;  // no group: this wave goes to the lane items
-            else
-                g = atomicAdd(&S.next_group, 1u);
-        }
+        if (lane == 0) g = atomicAdd(&S.next_group, 1u);
         return uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
     };
     const uint4* const listF = items + count + S.full_base;  // full pieces first
@@ -2917,24 +2896,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             d = d1;
         }
     };
-    // Lane items early (round 5): the last early_waves waves stop taking team
-    // groups when the list reaches items of <= early_rows rows, take the lane
-    // items (LDS-bound) beside the other waves' small groups (latency-bound),
-    // then return to the groups that are left.  The other waves go to the lane
-    // items when the groups run out, as before.
-    // Compiled in with MI_SORT_LANE_EARLY=1 only (A/B builds, with
-    // MI_SORT_LANE_BLOCKS=8: the second pass's registers spill at 16).
-#if MI_SORT_LANE_EARLY
-    const bool early_wave = early_waves && (threadIdx.x >> 6) >= kBlock / 64 - early_waves;
-    if (early_wave && S.small_base != 0xFFFFFFFFu) g_small = (n_full + S.small_base) / 8;
-    for (int pass = 0; pass < 2; ++pass)
-    {
-    grab_limited = pass == 0 && early_wave;
-#else
-    (void)early_waves;
-    (void)early_rows;
-    {
-#endif
     uint32_t g_cur = grab();
     uint4 d_cur = load_desc(g_cur);
     uint32_t g_nxt = grab();
@@ -3101,21 +3062,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
-#if MI_SORT_LANE_EARLY
-    if (pass == 0)
-    {
-        SORT_STAMP(5);
-        lane_items();
-        SORT_STAMP(6);
-    }
-    if (!early_wave) break;
-    }  // pass
-#else
     SORT_STAMP(5);
     lane_items();
     SORT_STAMP(6);
-    }
-#endif
     if (INLOOP) return;  // whole records were finished in the loop
     // Finish pass, in list order (round 5): a whole record's fold value W
     // (wr at its slot, eight consecutive words per group) is Z_m(raw) of its
@@ -3195,7 +3144,7 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base, ws.lane_early);
+                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base);
     return hipGetLastError();
 }
 

@@ -682,18 +682,6 @@ bool fused_ok(DeviceState* d, const Ctx* c, int grid)
     return grid <= d->cus && d->sorted_users.load() == 1;
 }
 
-// Waves that take the lane items early, and the item size that starts
-// them: MI_CRC32C_SORT_LANE_EARLY=waves[,rows] (A/B; default none).
-uint32_t sorted_lane_early()
-{
-    const char* e = std::getenv("MI_CRC32C_SORT_LANE_EARLY");
-    if (!e || !*e) return 0;
-    const int w = std::max(0, std::min(15, std::atoi(e)));
-    const char* c = std::strchr(e, ',');
-    const int r = c ? std::max(1, std::min(int(kSortLaneRowsMax) + 60, std::atoi(c + 1))) : 8;
-    return w ? (uint32_t(w) << 16) | uint32_t(r) : 0u;
-}
-
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
 int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
@@ -722,8 +710,7 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
                        reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
-                       sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base,
-                       sorted_lane_early()};
+                       sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base};
     // MI_CRC32C_SORT_BARRIER_SKEW=1 (tests): the kernel waits for one arrival
     // more than the grid has, so every workgroup's wait times out
     const char* skew = std::getenv("MI_CRC32C_SORT_BARRIER_SKEW");

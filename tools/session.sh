@@ -37,6 +37,11 @@ while [ $# -gt 0 ]; do
                echo "== $m"; python3 tools/pmc_summary.py "$OUT/fs_$m" crc32c_sorted_kernel sorted_cost_kernel
              done | tee -a "$OUT/fetchsplit.out"
              rm -rf "$OUT"/fs_*/ ;;
+    stealab) for rnd in 1 2 3; do for cfg in ${STEAL_CFGS:-r05d_0 head_0 head_4 head_8 head_16}; do
+               set -- ${cfg/_/ }; lib=tools/ab/libconsus_crc32c_$1.so; [ "$1" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
+               echo -n "round $rnd lib=$1 steal=$2 "; MI_CRC32C_SORT_STEAL=$2 timeout -k 10 120 python3 tools/zipf_probe.py $lib > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
+             done; done | tee "$OUT/stealab.out"
+             for v in ${STEAL_MID:-0 4 8}; do MI_CRC32C_SORT_STEAL=$v timeout -k 10 120 python3 tools/mid_probe.py --path sorted --mib 64,256 --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/steal=$v /"; done | tee -a "$OUT/stealab.out" ;;
     midhead) run mid_head 300 python3 -u tools/mid_probe.py --mib ${MID_MIB:-1,2,4,8,16,32,64,256} --reps 300 ;;
     winbig) for rnd in 1 2; do for cfg in "window 8 256" "window 16 256" "window 8 64" "sorted 0 0"; do
              set -- $cfg; MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 /"
@@ -141,9 +146,6 @@ while [ $# -gt 0 ]; do
              done
              echo -n "round $rnd zipf_probe: "; timeout -k 10 120 python3 tools/zipf_probe.py > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
              done | tee "$OUT/legcmp.out" ;;
-    earlyab) for rnd in 1 2 3; do for cfg in ${EARLY_CFGS:-"r05d 0" "lb8 0" "lb8 2" "lb8 4" "lb8 8"}; do
-               set -- $cfg; echo -n "round $rnd lib=$1 lane_early=$2 "; MI_CRC32C_SORT_LANE_EARLY=$2 timeout -k 10 120 python3 tools/zipf_probe.py tools/ab/libconsus_crc32c_$1.so > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
-             done; done | tee "$OUT/earlyab.out" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
