@@ -2039,6 +2039,8 @@ struct SortShared
     uint32_t full_base;        // their slots: items[count + full_base ...]
     uint32_t next_group;
     uint32_t next_lane;        // lane items taken (64 per grab)
+    uint32_t teams_done;       // waves whose team groups are done (finish overlap)
+    uint32_t next_fin;         // finish-pass records taken
     uint32_t lane_base;        // the first lane item's position among the last pieces
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
@@ -2443,6 +2445,9 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #ifndef MI_SORT_LANE_BLOCKS
 #define MI_SORT_LANE_BLOCKS 16
 #endif
+#ifndef MI_SORT_FIN_OVERLAP
+#define MI_SORT_FIN_OVERLAP 1
+#endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 #define SORT_STAMP(k)                                                                        \
@@ -2476,13 +2481,15 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x < 2) S.fbins[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.next_group = 0;
     if (threadIdx.x == 0) S.next_lane = 0;
+    if (threadIdx.x == 0) S.teams_done = 0;
+    if (threadIdx.x == 0) S.next_fin = 0;
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
     // whole records finished in the loop (RB = 4, small batches) or by the
     // finish pass (RB = 2, configs[2]: in the loop it measured 0.829-0.831
     // ms against 0.788-0.791, profiles/r04_configs2_variants_ab.txt)
     constexpr bool INLOOP = RB >= 4;
-    if (INLOOP) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
+    if (INLOOP || MI_SORT_FIN_OVERLAP) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     // (1) Wave 0: the two targets and the cost blocks holding them.  (The
     // tables are staged later, at the stage_tables() call after the binning
     // has written the descriptor list out: until then their LDS holds the
@@ -3062,6 +3069,13 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         step(vB, shB, vA, shA);
     }
     flush();
+#if MI_SORT_FIN_OVERLAP
+    // this wave's fold values (wr) are stored: count it done for the finish
+    // pass, which starts when every wave's team groups are, beside the other
+    // waves' lane items
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) atomicAdd(&S.teams_done, 1u);
+#endif
     SORT_STAMP(5);
     lane_items();
     SORT_STAMP(6);
@@ -3076,6 +3090,48 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // left in out[r] in record order, then wr[slot]: two dependent round
     // trips, and the binning pass stored every slot).  The CRCs go to out[rec],
     // scattered inside the workgroup's record range.
+#if MI_SORT_FIN_OVERLAP
+    // (round 5) No workgroup barrier: a wave whose lane items are done waits
+    // for every wave's team groups only (their wr stores), then takes records
+    // 256 at a time while other waves may still hash lane items.
+    while (__hip_atomic_load(&S.teams_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < kBlock / 64)
+        __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    constexpr uint32_t FU = 4;
+    const uint32_t n_whole = n_long - n_full;
+    const uint4* const dl = items + rlo;
+    for (;;)
+    {
+        uint32_t c0 = 0;
+        if (lane == 0) c0 = atomicAdd(&S.next_fin, FU * 64u);
+        c0 = uint32_t(__builtin_amdgcn_readfirstlane(int(c0)));
+        if (c0 >= n_whole) break;
+        uint4 dv[FU];
+        uint32_t wv[FU];
+#pragma unroll
+        for (uint32_t u = 0; u < FU; ++u)
+        {
+            const uint32_t k = c0 + u * 64 + lane;
+            dv[u] = k < n_whole ? dl[k] : make_uint4(0, 0, 0, kSortMulti);
+            wv[u] = k < n_whole ? wr[uint64_t(rlo) + k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < FU; ++u)
+        {
+            const uint64_t ps = uint64_t(dv[u].x) | (uint64_t(dv[u].y) << 32);
+            const uint32_t m = uint32_t(0u - uint32_t(ps + dv[u].z)) & 127u;
+            uint32_t v = wv[u];
+            const uint32_t n = 128u - m;
+            uint32_t t = zT_n(v, n & 15u);
+            t = (n & 16u) ? zT<4>(t) : t;
+            t = (n & 32u) ? zG(kLdsZ32, t) : t;
+            t = (n & 64u) ? zG(kLdsZ64, t) : t;
+            t = zG(kLdsZInv, t);
+            v = m ? t : v;
+            if (!(dv[u].w & kSortMulti)) out[dv[u].w & kSortRecMask] = ~v;
+        }
+    }
+#else
     S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     __syncthreads();  // the workgroup's own stores are visible to it past the barrier
     constexpr uint32_t FU = 4;
@@ -3108,6 +3164,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             if (!(dv[u].w & kSortMulti)) out[dv[u].w & kSortRecMask] = ~v;
         }
     }
+#endif
     SORT_STAMP(7);
 }
 
