@@ -1956,7 +1956,12 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 
 // Two or four cost blocks per launch block, every load issued first, gave
 // kernel minimums of 6.2 and 6.5 us against 7.2 but did not move the step
-// (5 interleaved rounds, profiles/r02_sorted_cost_kernel_ab.txt).
+// (5 interleaved rounds, profiles/r02_sorted_cost_kernel_ab.txt).  Round 5,
+// on the current hash kernel: two per launch block took configs[2] (1,024
+// cost blocks) 1-2 us faster (better in 7 of 8 interleaved pairs) and 64 /
+// 256 MiB batches (15-58 cost blocks) 0.3-0.5 us slower; four was mixed
+// (profiles/r05_cost_blocks_ab.txt).  So X = 2 from 512 cost blocks on.
+template <uint32_t X>
 __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint64_t count,
@@ -1964,7 +1969,6 @@ __global__ __launch_bounds__(kPlanThreads) void sorted_cost_kernel(
     const uint32_t* __restrict__ tables, uint32_t plog)
 {
     static_assert(kSortPer == 1, "one record per thread and cost block");
-    constexpr uint32_t X = 1;
     __shared__ uint64_t sh[X][kPlanThreads / 64];
     uint64_t av[X];
     uint32_t Lv[X];
@@ -3196,8 +3200,12 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     const uint32_t nb = sorted_blocks(count);
     const uint8_t* b = static_cast<const uint8_t*>(base);
     if (!ws.fused)
-        hipLaunchKernelGGL(sorted_cost_kernel, dim3(nb), dim3(kPlanThreads), 0, stream, b, offsets,
+    {
+        const uint32_t X = nb >= 512 ? 2u : 1u;
+        auto ck = X == 2 ? sorted_cost_kernel<2> : sorted_cost_kernel<1>;
+        hipLaunchKernelGGL(ck, dim3((nb + X - 1) / X), dim3(kPlanThreads), 0, stream, b, offsets,
                            lengths, inits, count, ws.blk_cost, ws.ctrl, out, tables, ws.plog);
+    }
     auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,

@@ -41,7 +41,7 @@ while [ $# -gt 0 ]; do
                set -- ${cfg/_/ }; lib=tools/ab/libconsus_crc32c_$1.so; [ "$1" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
                echo -n "round $rnd lib=$1 steal=$2 "; MI_CRC32C_SORT_STEAL=$2 timeout -k 10 120 python3 tools/zipf_probe.py $lib > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
              done; done | tee "$OUT/stealab.out"
-             for v in ${STEAL_MID:-0 4 8}; do MI_CRC32C_SORT_STEAL=$v timeout -k 10 120 python3 tools/mid_probe.py --path sorted --mib 64,256 --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/steal=$v /"; done | tee -a "$OUT/stealab.out" ;;
+             for v in ${STEAL_MID:-0 4 8}; do MI_CRC32C_SORT_STEAL=$v timeout -k 10 120 python3 tools/mid_probe.py --path sorted --mib 64,256 --reps 200 ${MID_LIB:+--lib $MID_LIB} > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/steal=$v /"; done | tee -a "$OUT/stealab.out" ;;
     midhead) run mid_head 300 python3 -u tools/mid_probe.py --mib ${MID_MIB:-1,2,4,8,16,32,64,256} --reps 300 ;;
     winbig) for rnd in 1 2; do for cfg in "window 8 256" "window 16 256" "window 8 64" "sorted 0 0"; do
              set -- $cfg; MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 /"
