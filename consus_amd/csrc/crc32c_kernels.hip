@@ -2049,6 +2049,7 @@ struct SortShared
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
     uint32_t bar_ok;           // fused launch: the grid barrier completed
+    uint32_t sink;             // prefetch results' sink (never written in practice)
     uint64_t pre[2];           // cost before those blocks
     uint64_t target[2];
     uint64_t total;            // the batch's total cost C
@@ -2452,6 +2453,9 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #ifndef MI_SORT_FIN_OVERLAP
 #define MI_SORT_FIN_OVERLAP 1
 #endif
+#ifndef MI_SORT_PREFETCH
+#define MI_SORT_PREFETCH 1
+#endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 #define SORT_STAMP(k)                                                                        \
@@ -2502,7 +2506,34 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (fused && !sorted_fused_costs(base, off, len, inits, count, blk_cost, nb, ctrl, out, tables,
                                      plog, bar_base, S))
         return;  // the grid barrier timed out: ctrl[3] tells the host (below)
-    if (threadIdx.x < 64) sort_find_blocks(blk_cost, nb, count, S);
+    if (threadIdx.x < 64)
+        sort_find_blocks(blk_cost, nb, count, S);
+#if MI_SORT_PREFETCH
+    else
+    {
+        // (round 5) While wave 0 searches the cost blocks, the other waves
+        // read the middle of this workgroup's likely record range (the
+        // record-count share: a cost share is near it) so that the binning
+        // pass's offset and length loads hit L2.
+        const uint64_t per = count / gridDim.x;
+        const uint64_t r0 = uint64_t(blockIdx.x) * per + per / 8;
+        const uint64_t re = r0 + per - per / 4;
+        constexpr uint32_t PF = 4;  // records per thread, every load issued first
+        uint64_t o[PF];
+        uint32_t l[PF];
+#pragma unroll
+        for (uint32_t u = 0; u < PF; ++u)
+        {
+            const uint64_t r = r0 + threadIdx.x - 64 + u * (kBlock - 64);
+            o[u] = r < re ? off[r] : 0;
+            l[u] = r < re ? len[r] : 0;
+        }
+        uint64_t acc = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < PF; ++u) acc += o[u] + l[u];
+        if (acc == 0x5A5A5A5A5A5A5A5Aull) S.sink = uint32_t(acc);
+    }
+#endif
     __syncthreads();
     SORT_STAMP(1);
     // The tables are staged after the binning (step 3), which uses their LDS
