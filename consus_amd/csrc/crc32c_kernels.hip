@@ -1885,8 +1885,13 @@ constexpr uint32_t kSortBins = kSortRows + 7 * kSortLaneRowsMax;
 // less (A/B against equal shares: 0.878-0.905 ms vs 0.885-0.916 at 20;
 // 15 is the default, 0 turns it off).
 // (round 4, with the edge-row policy: 0 / 30 measured 0.796-0.797 /
-// 0.792-0.793 ms against 0.788-0.791 at 15, profiles/r04_configs2_variants_ab.txt)
-constexpr uint32_t kSortXcdw = 15;
+// 0.792-0.793 ms against 0.788-0.791 at 15, profiles/r04_configs2_variants_ab.txt;
+// round 5, final kernel: 0 / 30 0.772-0.774 / 0.768-0.769 against 0.765 at
+// 15, profiles/r05_xcd_weight_lane_rows_ab.txt; MI_SORT_XCDW builds A/B variants)
+#ifndef MI_SORT_XCDW
+#define MI_SORT_XCDW 15
+#endif
+constexpr uint32_t kSortXcdw = MI_SORT_XCDW;
 constexpr uint32_t kSortFold = 2;            // cost allowance per item, in rows (fold, masks)
 constexpr uint32_t kSortPer = 1;             // records per thread of a cost block
 constexpr uint32_t kSortRecs = kPlanThreads * kSortPer;
