@@ -1892,7 +1892,10 @@ constexpr uint32_t kSortBins = kSortRows + 7 * kSortLaneRowsMax;
 #define MI_SORT_XCDW 15
 #endif
 constexpr uint32_t kSortXcdw = MI_SORT_XCDW;
-constexpr uint32_t kSortFold = 2;            // cost allowance per item, in rows (fold, masks)
+#ifndef MI_SORT_FOLD_COST
+#define MI_SORT_FOLD_COST 2
+#endif
+constexpr uint32_t kSortFold = MI_SORT_FOLD_COST;            // cost allowance per item, in rows (fold, masks)
 constexpr uint32_t kSortPer = 1;             // records per thread of a cost block
 constexpr uint32_t kSortRecs = kPlanThreads * kSortPer;
 constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a split record
