@@ -225,3 +225,40 @@ def test_window_host_batch_with_long_records(engine, oracle):
     got = engine.crc32c_batch(buf, offsets, lengths)
     assert np.array_equal(got, oracle.batch(buf, offsets, lengths))
     assert engine.stats()["window_batches"] == before + 1
+
+
+def test_window_concurrent_threads(engine, oracle):
+    """Eight threads, each with its own engine context (stream and acc
+    words), run window-path batches with records split over several waves
+    at once; every result exact, and every context's words left zero (the
+    second batch of each thread checks that)."""
+    import threading
+    errors = []
+
+    def worker(t):
+        r = np.random.default_rng(300 + t)
+        try:
+            for _ in range(2):
+                count = int(r.integers(50, 1500))
+                lengths = r.integers(0, 20_000, count).astype(np.uint32)  # <= 24 MiB a batch
+                offsets, end = _packed(r, lengths, gap=5, start=int(r.integers(0, 128)))
+                buf = r.integers(0, 256, end + 16, dtype=np.uint8)
+                inits = r.integers(0, 2**32, count, dtype=np.uint32)
+                b = _Batch(engine, buf, offsets, lengths, inits)
+                try:
+                    if not np.array_equal(b.run(), oracle.batch(buf, offsets, lengths, inits, threads=1)):
+                        errors.append(("mismatch", t, count))
+                finally:
+                    b.free()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(("exception", t, repr(e)))
+
+    assert "MI_CRC32C_VARPATH" not in os.environ
+    before = engine.stats()["window_batches"]
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+    assert engine.stats()["window_batches"] >= before + 16
