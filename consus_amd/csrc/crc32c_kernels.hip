@@ -3514,7 +3514,7 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
     }
 }
 
-size_t window_lds_bytes(uint32_t count) { return size_t(count) * 4 + 4 * (kWinBlockMax / 64); }
+size_t window_lds_bytes(uint32_t count) { return size_t(count) * 4 + 4 * (kWinBlockBig / 64); }
 
 uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_t block, uint32_t rows)
 {
@@ -3531,23 +3531,40 @@ hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32
                          hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
-    if (count > kWinMaxCount) return hipErrorInvalidValue;
-    // one-wave workgroups spread a small batch's lane-table permutes over as
-    // many CUs as it has waves; 4-wave ones read the lengths fewer times
-    if (block == 0) block = count <= kWinSmallCount ? 64u : kWinBlockMax;
+    if (count > kWinMaxCountBig) return hipErrorInvalidValue;
     // 4-row windows up to 12 waves of them per CU (grid_cap / 8 = the CUs),
     // then 8: configs[2] records cut to 1 / 2 / 4 / 8 / 16 MiB took 7.2 / 8.4
     // / 9.3 / 12.6 / 21.5 us with 4 rows, 8.7 / 9.7 / 10.2 / 13.8 / 17.4 with 8,
     // 12.0 / 12.8 / 13.8 / 15.0 / 20.3 with 16 (profiles/r05_window_rows.txt)
-    if (rows == 0)
-        rows = window_grid(count, total_bytes, 1 << 30, 64, 4) <= 12 * (uint64_t(grid_cap) / 8) ? 4u : 8u;
-    const uint32_t g = uint32_t(window_grid(count, total_bytes, grid_cap, block, rows));
-    auto k = block == 64 ? (rows == 4   ? crc32c_window_kernel<64, 4>
-                            : rows == 8 ? crc32c_window_kernel<64, 8>
-                                        : crc32c_window_kernel<64, 16>)
-                         : (rows == 4   ? crc32c_window_kernel<kWinBlockMax, 4>
-                            : rows == 8 ? crc32c_window_kernel<kWinBlockMax, 8>
-                                        : crc32c_window_kernel<kWinBlockMax, 16>);
+    const uint64_t cus = uint64_t(grid_cap) / 8;
+    if (rows == 0) rows = window_grid(count, total_bytes, 1 << 30, 64, 4) <= 12 * cus ? 4u : 8u;
+    // One-wave workgroups spread a small batch's lane-table permutes over as
+    // many CUs as it has waves; four-wave ones read the lengths fewer times;
+    // one twelve-wave workgroup per CU (kWinBlockBig) builds the prefix once
+    // per CU, which pays once the windows fill most of the CUs' teams: 4-row
+    // windows above 48 per CU, 8-row ones from 64 up to ~1.1 rounds of 96 per
+    // CU (a second round costs ~11 us).  configs[2] cut to 8 / 16 / 20 MiB:
+    // 11.6 / 15.9 / 16.8 us against 12.6 / 17.5 / 20.0 with four-wave
+    // workgroups; at 4 / 12 / 24 MiB the four-wave ones were faster
+    // (profiles/r05_window_block768.txt)
+    if (block == 0)
+    {
+        const uint64_t w = window_grid(count, total_bytes, 1 << 30, kTeam, rows);  // windows
+        const bool big = rows == 4 ? w > 48 * cus : (w > 64 * cus && w <= 108 * cus);
+        block = big ? kWinBlockBig : count <= kWinSmallCount ? 64u : kWinBlockMax;
+    }
+    // kWinBlockBig workgroups: one per CU (grid_cap / 8), looping over the windows
+    const uint32_t g = uint32_t(window_grid(count, total_bytes, block == kWinBlockBig ? grid_cap / 8 : grid_cap,
+                                            block, rows));
+    auto k = block == 64             ? (rows == 4   ? crc32c_window_kernel<64, 4>
+                                        : rows == 8 ? crc32c_window_kernel<64, 8>
+                                                    : crc32c_window_kernel<64, 16>)
+             : block == kWinBlockBig ? (rows == 4   ? crc32c_window_kernel<kWinBlockBig, 4>
+                                        : rows == 8 ? crc32c_window_kernel<kWinBlockBig, 8>
+                                                    : crc32c_window_kernel<kWinBlockBig, 16>)
+                                     : (rows == 4   ? crc32c_window_kernel<kWinBlockMax, 4>
+                                        : rows == 8 ? crc32c_window_kernel<kWinBlockMax, 8>
+                                                    : crc32c_window_kernel<kWinBlockMax, 16>);
     hipLaunchKernelGGL(k, dim3(g), dim3(block), window_lds_bytes(uint32_t(count)), stream,
                        static_cast<const uint8_t*>(base), offsets, lengths, inits, uint32_t(count),
                        out, acc64, acc, cnt, tables, pow2);
@@ -3584,11 +3601,14 @@ hipError_t configure_kernels()
                         reinterpret_cast<const void*>(&crc32c_window_kernel<64, 8>),
                         reinterpret_cast<const void*>(&crc32c_window_kernel<64, 16>),
                         reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockMax, 8>),
-                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockMax, 16>)};
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockMax, 16>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockBig, 4>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockBig, 8>),
+                        reinterpret_cast<const void*>(&crc32c_window_kernel<kWinBlockBig, 16>)};
     for (const void* f : kw)
         if (e == hipSuccess)
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    int(window_lds_bytes(kWinMaxCount)));
+                                    int(window_lds_bytes(kWinMaxCountBig)));
     const void* ks[] = {reinterpret_cast<const void*>(&crc32c_sorted_kernel<2>),
                         reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>)};
     for (const void* f : ks)

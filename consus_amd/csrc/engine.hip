@@ -586,15 +586,18 @@ int varpath_forced()
 // batches of at most kWinMaxCount records and kWinMaxBytes bytes (total
 // given); MI_CRC32C_VARPATH=window forces it up to kWinMaxCount records,
 // =sorted / =pieces never.  MI_CRC32C_WIN_MAX_BYTES overrides the size bound
-// (probes; read per batch).  configs[2] records cut to 16 / 32 MiB (3811 /
-// 7481 records): 17.4 / 30.7 us against the sorted path's 25.3 / 27.5
-// (profiles/r05_window_vs_sorted_large.txt); the record bound (4096) ends the
-// window path first for such batches.
+// (probes; read per batch), MI_CRC32C_WIN_MAX_COUNT the record bound (up to
+// kWinMaxCountBig).  configs[2] records cut to 16 / 20 / 24 / 28 MiB (3811 /
+// 4727 / 5687 / 6513 records): 15.9 / 16.8 / 24.3 / 26.5 us against the
+// sorted path's 24.7 / 25.4 / 25.7 / 26.3 (profiles/r05_window_block768.txt).
 constexpr uint64_t kWinMaxBytes = 24ull << 20;
 bool window_path(uint64_t count, uint64_t total_bytes)
 {
     const int f = varpath_forced();
-    if (!total_bytes || count > kWinMaxCount || f == 1 || f == 2) return false;
+    uint64_t maxc = kWinMaxCount;  // MI_CRC32C_WIN_MAX_COUNT (probes), up to kWinMaxCountBig
+    if (const char* e = std::getenv("MI_CRC32C_WIN_MAX_COUNT"))
+        maxc = std::min<uint64_t>(kWinMaxCountBig, std::strtoull(e, nullptr, 10));
+    if (!total_bytes || count > maxc || f == 1 || f == 2) return false;
     if (f == 3) return true;
     uint64_t cap = kWinMaxBytes;
     if (const char* e = std::getenv("MI_CRC32C_WIN_MAX_BYTES")) cap = std::strtoull(e, nullptr, 10);
@@ -734,7 +737,7 @@ int run_window(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     // MI_CRC32C_WIN_BLOCK=64|256, MI_CRC32C_WIN_ROWS=4|8|16: the workgroup and
     // the window (A/B, tests; default by count and size)
     uint32_t block = 0, rows = 0;
-    if (const char* e = std::getenv("MI_CRC32C_WIN_BLOCK")) block = std::atoi(e) == 64 ? 64u : 256u;
+    if (const char* e = std::getenv("MI_CRC32C_WIN_BLOCK")) block = std::atoi(e) == 64 ? 64u : std::atoi(e) == int(kWinBlockBig) ? kWinBlockBig : 256u;
     if (const char* e = std::getenv("MI_CRC32C_WIN_ROWS"))
         rows = std::atoi(e) == 4 ? 4u : std::atoi(e) == 8 ? 8u : 16u;
     HIP_TRY(launch_window(base, off, len, inits, count, total_bytes, out, acc64, acc, acc + count,

@@ -1,5 +1,5 @@
 """GPU parity of the window path (crc32c_kernels.hip "window path", DESIGN.md
-section 4.9): mid-size device batches (at most kWinMaxCount = 4096 records,
+section 4.9): mid-size device batches (at most kWinMaxCount = 8192 records,
 24 MiB by default) in one launch.  Each record is cut into windows of 16
 rows (2 KiB; 8 rows while the batch has fewer waves of them than the chip
 has CUs) counted back from its end, one window per team; a record of
@@ -7,9 +7,10 @@ several windows is combined through acc[] / cnt[] (XOR and count, the last
 team stores the CRC and zeroes both).  Every result is compared with the
 CPU oracle, bit-exact; the path is checked to have run
 (mi_crc32c_stats().window_batches).  MI_CRC32C_VARPATH=window forces the path
-up to 4096 records; without it, the engine takes it by size.  Each forced
+up to 8192 records; without it, the engine takes it by size.  Each forced
 test runs with the workgroup and window the engine picks by count and size,
-and with one-wave / four-wave workgroups (MI_CRC32C_WIN_BLOCK) and 8 / 16-row
+and with one-wave / four-wave / one-per-CU twelve-wave workgroups
+(MI_CRC32C_WIN_BLOCK=64 / 256 / 768) and 8 / 16-row
 windows (MI_CRC32C_WIN_ROWS, also 4) forced.
 """
 import os
@@ -21,9 +22,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(params=[{}, {"MI_CRC32C_WIN_BLOCK": "64"}, {"MI_CRC32C_WIN_BLOCK": "256"},
+                        {"MI_CRC32C_WIN_BLOCK": "768"},
                         {"MI_CRC32C_WIN_ROWS": "4"}, {"MI_CRC32C_WIN_ROWS": "8"},
                         {"MI_CRC32C_WIN_ROWS": "16"}],
-                ids=["by_size", "block_64", "block_256", "rows_4", "rows_8", "rows_16"])
+                ids=["by_size", "block_64", "block_256", "block_768", "rows_4", "rows_8", "rows_16"])
 def window_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "window"
@@ -139,9 +141,9 @@ def test_window_overlapping_and_unordered_records(engine, oracle, window_path):
     assert window_path() == 1
 
 
-@pytest.mark.parametrize("count", [1, 2, 4095, 4096])
+@pytest.mark.parametrize("count", [1, 2, 4095, 4096, 8191, 8192])
 def test_window_record_counts(engine, oracle, window_path, count):
-    """One record to the 4096-record LDS bound."""
+    """One record to the 8192-record bound."""
     rng = np.random.default_rng(count)
     lengths = rng.integers(0, 6000, count).astype(np.uint32)
     offsets, end = _packed(rng, lengths, start=3)
@@ -151,15 +153,32 @@ def test_window_record_counts(engine, oracle, window_path, count):
 
 
 def test_window_above_the_count_bound_takes_the_sorted_path(engine, oracle, window_path):
-    """4097 records: the window path declines even when forced."""
-    rng = np.random.default_rng(4097)
-    lengths = rng.integers(0, 3000, 4097).astype(np.uint32)
+    """8193 records: the window path declines even when forced."""
+    rng = np.random.default_rng(8193)
+    lengths = rng.integers(0, 3000, 8193).astype(np.uint32)
     offsets, end = _packed(rng, lengths)
     buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
     before = engine.stats()["sorted_batches"]
     _check(engine, oracle, buf, offsets, lengths)
     assert window_path() == 0
     assert engine.stats()["sorted_batches"] == before + 1
+
+
+@pytest.mark.parametrize("count", [8193, 12000, 16384, 16385])
+def test_window_raised_count_bound(engine, oracle, window_path, count):
+    """MI_CRC32C_WIN_MAX_COUNT raises the record bound up to the 64 KiB LDS
+    prefix (16384 records); 16385 records decline."""
+    rng = np.random.default_rng(count)
+    lengths = rng.integers(0, 4000, count).astype(np.uint32)
+    offsets, end = _packed(rng, lengths, gap=2, start=5)
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, count, dtype=np.uint32)
+    os.environ["MI_CRC32C_WIN_MAX_COUNT"] = "100000"  # clamped to 16384
+    try:
+        _check(engine, oracle, buf, offsets, lengths, inits)
+    finally:
+        del os.environ["MI_CRC32C_WIN_MAX_COUNT"]
+    assert window_path() == (1 if count <= 16384 else 0)
 
 
 @pytest.mark.parametrize("hint", [1, 4096])
@@ -200,12 +219,13 @@ def test_window_empty_records_only(engine, oracle, window_path):
 
 
 def test_window_default_routing_by_size(engine, oracle):
-    """Without MI_CRC32C_VARPATH: a 1 MiB and a 16 MiB configs[2]-like batch
-    (Zipf 64 B - 64 KiB) take the window path, one of 4200 records (20 MiB)
-    the sorted path."""
+    """Without MI_CRC32C_VARPATH: configs[2]-like batches (Zipf 64 B - 64 KiB)
+    of 1 / 8 / 16 / 20 MiB take the window path (four-wave, one-per-CU, ...
+    workgroups by size), one of 6513 records (28 MiB) the sorted path."""
     assert "MI_CRC32C_VARPATH" not in os.environ
     rng = np.random.default_rng(13)
-    for count, path in ((230, "window_batches"), (3811, "window_batches"), (4200, "sorted_batches")):
+    for count, path in ((230, "window_batches"), (1961, "window_batches"), (3811, "window_batches"),
+                        (4727, "window_batches"), (6513, "sorted_batches")):
         lengths = engine.zipf_lengths(0xDA7A5EED, count).astype(np.uint32)
         offsets, end = _packed(rng, lengths)
         buf = rng.integers(0, 256, end + 16, dtype=np.uint8)

@@ -42,9 +42,13 @@ while [ $# -gt 0 ]; do
                echo -n "round $rnd lib=$1 steal=$2 "; MI_CRC32C_SORT_STEAL=$2 timeout -k 10 120 python3 tools/zipf_probe.py $lib > "$OUT/z.out" 2>&1 || { cat "$OUT/z.out"; exit 1; }; tail -1 "$OUT/z.out"
              done; done | tee "$OUT/stealab.out"
              for v in ${STEAL_MID:-0 4 8}; do MI_CRC32C_SORT_STEAL=$v timeout -k 10 120 python3 tools/mid_probe.py --path sorted --mib 64,256 --reps 200 ${MID_LIB:+--lib $MID_LIB} > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/steal=$v /"; done | tee -a "$OUT/stealab.out" ;;
+    midab) for rnd in 1 2 3; do for v in ${MIDAB_LIBS:-pre768 head}; do
+             lib=tools/ab/libconsus_crc32c_$v.so; [ "$v" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
+             timeout -k 10 120 python3 tools/mid_probe.py --lib $lib --mib ${MID_MIB:-1,2,4,8,12,16,20,24,28} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd $v /"
+           done; done | tee "$OUT/midab.out" ;;
     midhead) run mid_head 300 python3 -u tools/mid_probe.py --mib ${MID_MIB:-1,2,4,8,16,32,64,256} --reps 300 ;;
-    winbig) for rnd in 1 2; do for cfg in "window 8 256" "window 16 256" "window 8 64" "sorted 0 0"; do
-             set -- $cfg; MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 /"
+    winbig) for rnd in 1 2; do for cfg in ${WINBIG_CFGS:-"window_8_256" "window_16_256" "window_8_64" "sorted_0_0"}; do
+             set -- ${cfg//_/ }; MI_CRC32C_WIN_MAX_COUNT=16384 MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 /"
            done; done | tee "$OUT/winbig.out" ;;
     winrows) for rnd in 1 2; do for r in ${WIN_ROWS:-4 8 16}; do
              MI_CRC32C_WIN_ROWS=$r timeout -k 10 120 python3 tools/mid_probe.py --path window --mib ${WIN_MIB:-1,2,4} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$r /"
