@@ -48,7 +48,7 @@ while [ $# -gt 0 ]; do
            done; done | tee "$OUT/midab.out" ;;
     midhead) run mid_head 300 python3 -u tools/mid_probe.py --mib ${MID_MIB:-1,2,4,8,16,32,64,256} --reps 300 ;;
     winbig) for rnd in 1 2; do for cfg in ${WINBIG_CFGS:-"window_8_256" "window_16_256" "window_8_64" "sorted_0_0"}; do
-             set -- ${cfg//_/ }; MI_CRC32C_WIN_MAX_COUNT=16384 MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 /"
+             set -- ${cfg//_/ }; MI_CRC32C_WIN_PIPE=${4:-0} MI_CRC32C_WIN_MAX_COUNT=16384 MI_CRC32C_WIN_ROWS=$2 MI_CRC32C_WIN_BLOCK=$3 timeout -k 10 120 python3 tools/mid_probe.py --path $1 --mib ${WIN_MIB:-16,32,48,64} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$2 block=$3 pipe=${4:-0} /"
            done; done | tee "$OUT/winbig.out" ;;
     winrows) for rnd in 1 2; do for r in ${WIN_ROWS:-4 8 16}; do
              MI_CRC32C_WIN_ROWS=$r timeout -k 10 120 python3 tools/mid_probe.py --path window --mib ${WIN_MIB:-1,2,4} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd rows=$r /"
