@@ -120,6 +120,18 @@ while [ $# -gt 0 ]; do
              done ;;
     zc) run zc_probe 120 python3 tools/zc_probe.py ;;
     mid) for pth in pieces sorted; do run mid_$pth 300 python3 -u tools/mid_probe.py --path $pth --mib ${MID_MIB:-1,4,16,64,256} --reps 200 || exit 1; done ;;
+    winfetch) C="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+             for m in ${WIN_MIB:-1 16 20}; do
+               (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/wf_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --mib $m --reps 20 > "$OUT/wf_$m.log" 2>&1) || { tail -20 "$OUT/wf_$m.log"; exit 1; }
+               echo "== $m MiB"; python3 tools/pmc_summary.py "$OUT/wf_$m" window_kernel; rm -rf "$OUT/wf_$m"
+             done | tee "$OUT/winfetch.out" ;;
+    winprof) for m in ${WIN_MIB:-1 16 20}; do
+               (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/wp_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --mib $m --reps 100 > "$OUT/wp_$m.log" 2>&1) || { tail -20 "$OUT/wp_$m.log"; exit 1; }
+               find "$OUT/wp_$m" -name '*kernel_stats.csv' -exec cp {} "$OUT/window_${m}mib_kernel_stats.csv" \;
+               rm -rf "$OUT/wp_$m"; echo "== $m MiB"; grep -v "^path" "$OUT/wp_$m.log" | tail -2; head -3 "$OUT/window_${m}mib_kernel_stats.csv" | cut -c1-200
+               (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/wpm_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --mib $m --reps 20 > "$OUT/wpm_$m.log" 2>&1) || { tail -20 "$OUT/wpm_$m.log"; exit 1; }
+               echo "== $m MiB FETCH_SIZE (KiB, per dispatch, median; x2 gfx950 correction not applied)"; python3 tools/pmc_summary.py "$OUT/wpm_$m" window_kernel; rm -rf "$OUT/wpm_$m"
+             done | tee "$OUT/winprof.out" ;;
     midprof) for pth in ${MID_PATHS:-pieces sorted}; do
                (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/midprof_$pth" -o k -- python3 "$ROOT/tools/mid_probe.py" --path $pth --mib ${MID_MIB:-64} --reps 50 > "$OUT/midprof_$pth.log" 2>&1) || { tail -20 "$OUT/midprof_$pth.log"; exit 1; }
                find "$OUT/midprof_$pth" -name '*kernel_trace.csv' -exec python3 "$ROOT/tools/kernel_gaps.py" {} 300 \; > "$OUT/midprof_${pth}_trace.txt" 2>&1
