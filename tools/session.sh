@@ -120,6 +120,11 @@ while [ $# -gt 0 ]; do
              done ;;
     zc) run zc_probe 120 python3 tools/zc_probe.py ;;
     mid) for pth in pieces sorted; do run mid_$pth 300 python3 -u tools/mid_probe.py --path $pth --mib ${MID_MIB:-1,4,16,64,256} --reps 200 || exit 1; done ;;
+    adaptab) for rnd in 1 2 3 4; do for cfg in ${ADAPT_SET:-head:1 head:0}; do
+               v=${cfg%%:*}; a=${cfg##*:}; lib=tools/ab/libconsus_crc32c_$v.so; [ "$v" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
+               r=$(MI_CRC32C_SORT_ADAPT=$a timeout -k 10 120 python3 tools/zipf_probe.py $lib 2>&1 | tail -1) || { echo "$r"; exit 1; }
+               echo "round $rnd $v adapt=$a $r"; case "$r" in *MISMATCH*) exit 1;; esac
+             done; done | tee "$OUT/adaptab.out" ;;
     winfetch) C="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
              for m in ${WIN_MIB:-1 16 20}; do
                (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/wf_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --mib $m --reps 20 > "$OUT/wf_$m.log" 2>&1) || { tail -20 "$OUT/wf_$m.log"; exit 1; }
