@@ -815,7 +815,7 @@ def run_mid(E, sizes_mib=(1, 4, 16, 20, 64, 256), reps: int = 200) -> dict:
     """Mid-size device batches (VERDICT r4 Next 4; a durable-log segment,
     /root/reference/txman/durable_log.cc:287-347): configs[2]'s record stream
     cut to N MiB, one batch per launch on the engine's own path choice (the
-    window path up to 24 MiB / 8192 records, the sorted path above), HIP
+    window path up to 26 MiB / 8192 records, the sorted path above), HIP
     events over `reps` back-to-back batches after a warm-up; every size's
     CRCs checked against the oracle (a checker, outside the timed region)."""
     from consus_amd import workload as W

@@ -590,7 +590,7 @@ int varpath_forced()
 // kWinMaxCountBig).  configs[2] records cut to 16 / 20 / 24 / 28 MiB (3811 /
 // 4727 / 5687 / 6513 records): 15.9 / 16.8 / 24.3 / 26.5 us against the
 // sorted path's 24.7 / 25.4 / 25.7 / 26.3 (profiles/r05_window_block768.txt).
-constexpr uint64_t kWinMaxBytes = 24ull << 20;
+constexpr uint64_t kWinMaxBytes = 26ull << 20;
 bool window_path(uint64_t count, uint64_t total_bytes)
 {
     const int f = varpath_forced();

@@ -299,7 +299,7 @@ def _device_run_no_hint(engine, buf, offsets, lengths):
 @pytest.mark.parametrize("mib", [1, 64, 300, 400])
 def test_sorted_default_with_known_total(engine, oracle, mib):
     """Without the knob, a device batch whose total is given takes the sorted
-    path above 24 MiB or 8192 records (round 4: with batch-sized pieces it is
+    path above 26 MiB or 8192 records (round 4: with batch-sized pieces it is
     the faster path from 1 MiB up; round 5: below that bound the one-launch
     window path, tests/test_gpu_window.py); without the total, the piece path
     (its plan reads the item count back)."""
@@ -310,7 +310,7 @@ def test_sorted_default_with_known_total(engine, oracle, mib):
     offsets, end = _packed(rng, lengths)
     buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
     want = oracle.batch(buf, offsets, lengths)
-    path = "window_batches" if end <= (24 << 20) and count <= 8192 else "sorted_batches"
+    path = "window_batches" if end <= (26 << 20) and count <= 8192 else "sorted_batches"
     before = engine.stats()[path]
     assert np.array_equal(_device_run(engine, buf, offsets, lengths), want)
     assert engine.stats()[path] == before + 1

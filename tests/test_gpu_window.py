@@ -1,10 +1,10 @@
 """GPU parity of the window path (crc32c_kernels.hip "window path", DESIGN.md
 section 4.9): mid-size device batches (at most kWinMaxCount = 8192 records,
-24 MiB by default) in one launch.  Each record is cut into windows of 16
-rows (2 KiB; 8 rows while the batch has fewer waves of them than the chip
-has CUs) counted back from its end, one window per team; a record of
-several windows is combined through acc[] / cnt[] (XOR and count, the last
-team stores the CRC and zeroes both).  Every result is compared with the
+26 MiB by default) in one launch.  Each record is cut into windows of 4, 8
+or 16 rows (512 B - 2 KiB, by batch size) counted back from its end, one
+window per team; a record over several waves is combined through one 64-bit
+word per record (XOR and segment mask; acc[] / cnt[] past 32 segments), the
+last segment storing the CRC and zeroing the words.  Every result is compared with the
 CPU oracle, bit-exact; the path is checked to have run
 (mi_crc32c_stats().window_batches).  MI_CRC32C_VARPATH=window forces the path
 up to 8192 records; without it, the engine takes it by size.  Each forced
@@ -260,7 +260,7 @@ def test_window_concurrent_threads(engine, oracle):
         try:
             for _ in range(2):
                 count = int(r.integers(50, 1500))
-                lengths = r.integers(0, 20_000, count).astype(np.uint32)  # <= 24 MiB a batch
+                lengths = r.integers(0, 20_000, count).astype(np.uint32)  # <= 26 MiB a batch
                 offsets, end = _packed(r, lengths, gap=5, start=int(r.integers(0, 128)))
                 buf = r.integers(0, 256, end + 16, dtype=np.uint8)
                 inits = r.integers(0, 2**32, count, dtype=np.uint32)
