@@ -2,7 +2,8 @@
 variable-length entry point: host batches on the direct kernel and on the
 planned path, device batches with and without the size hint, fixed-stride
 batches (also split over 2-5 ranges through the multi-device entry
-points), the sorted path at random grids, the direct kernel's two forms
+points), the sorted path at random grids, the window path at random
+workgroups and windows, the direct kernel's two forms
 and its zero-copy read from pinned memory, and single buffers (host and
 device).  Shapes mix empty, tiny,
 row- and chunk-edge, and multi-chunk records; offsets packed, random,
@@ -121,6 +122,28 @@ def test_fuzz_round(engine, oracle, round_):
         os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
         os.environ.pop("MI_CRC32C_SORT_RING", None)
         os.environ.pop("MI_CRC32C_SORT_LANE_ROWS", None)
+
+    # the window path forced (count < 3000 is inside its record bound), at a
+    # random workgroup (one wave, four, one twelve-wave workgroup per CU) and
+    # window (4 / 8 / 16 rows), with the hint or an understated one (looping)
+    block = [None, "64", "256", "768"][int(rng.integers(0, 4))]
+    rows = [None, "4", "8", "16"][int(rng.integers(0, 4))]
+    os.environ["MI_CRC32C_VARPATH"] = "window"
+    if block:
+        os.environ["MI_CRC32C_WIN_BLOCK"] = block
+    if rows:
+        os.environ["MI_CRC32C_WIN_ROWS"] = rows
+    try:
+        before = engine.stats()["window_batches"]
+        hint = max(int(lengths.sum(dtype=np.uint64)), 1) if rng.integers(0, 4) else 1
+        d_out.upload(np.full(count, 0xABABABAB, dtype=np.uint32))
+        engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini, total_bytes=hint)
+        assert np.array_equal(d_out.download(np.uint32, count), want), ("window", block, rows, hint)
+        assert engine.stats()["window_batches"] == before + 1
+    finally:
+        os.environ.pop("MI_CRC32C_VARPATH", None)
+        os.environ.pop("MI_CRC32C_WIN_BLOCK", None)
+        os.environ.pop("MI_CRC32C_WIN_ROWS", None)
 
     # single buffers: one record on the host and on the device
     i = int(rng.integers(0, count))
