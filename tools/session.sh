@@ -120,6 +120,9 @@ while [ $# -gt 0 ]; do
              done ;;
     zc) run zc_probe 120 python3 tools/zc_probe.py ;;
     mid) for pth in pieces sorted; do run mid_$pth 300 python3 -u tools/mid_probe.py --path $pth --mib ${MID_MIB:-1,4,16,64,256} --reps 200 || exit 1; done ;;
+    piecesweep) for rnd in 1 2; do for pl in ${SWEEP_PLOG:-13 14 15 16}; do for rg in ${SWEEP_RING:-4 2}; do
+               MI_CRC32C_SORT_PIECE_LOG2=$pl MI_CRC32C_SORT_RING=$rg timeout -k 10 120 python3 tools/mid_probe.py --path sorted --mib ${MID_MIB:-128,256,512} --reps 100 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd plog=$pl ring=$rg /"
+             done; done; done | tee "$OUT/piecesweep.out" ;;
     adaptab) for rnd in 1 2 3 4; do for cfg in ${ADAPT_SET:-head:1 head:0}; do
                v=${cfg%%:*}; a=${cfg##*:}; lib=tools/ab/libconsus_crc32c_$v.so; [ "$v" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
                r=$(MI_CRC32C_SORT_ADAPT=$a timeout -k 10 120 python3 tools/zipf_probe.py $lib 2>&1 | tail -1) || { echo "$r"; exit 1; }
