@@ -633,12 +633,21 @@ int reserve_zeroed(DevBuf& b, size_t bytes, hipStream_t stream)
 // (4 against 2, ms per device batch: 1 MiB .027/.029, 16 MiB .031/.034,
 // 256 MiB .072/.074, 1 GiB .207/.218, 2 GiB .391/.395;
 // profiles/r04_sorted_ring_sweep.txt)
+// Re-measured on the round-5 kernel (4-row ring, us per batch;
+// profiles/r05_sorted_piece_sweep_recheck.txt):
+//   batch     32 MiB  64 MiB  96 MiB  128 MiB  160 MiB  192 MiB  256 MiB
+//   2 KiB     27.3    35.5    41.8    50.6     57.0     63.4
+//   4 KiB     27.4    31.5    37.6    45.9     52.6     58.9
+//   8 KiB     31.5    34.6    37.9    41.1     47.3     53.0     66.0
+//   16 KiB    43.0    43.8    46.5    46.1     48.1     53.1     63.6
+// so 8 KiB pieces from 112 MiB (128 MiB: 41.1 against 45.9) to 224 MiB.
 constexpr int kSortRingSmall = 4;
 
 uint32_t sorted_piece_log2(uint64_t total_bytes)
 {
     if (total_bytes < (uint64_t(32) << 20)) return 11;
-    if (total_bytes < (uint64_t(160) << 20)) return 12;
+    if (total_bytes < (uint64_t(112) << 20)) return 12;
+    if (total_bytes < (uint64_t(224) << 20)) return 13;
     if (total_bytes < (uint64_t(3) << 30)) return 14;
     return kSortPieceLog2;
 }
