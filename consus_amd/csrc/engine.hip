@@ -641,6 +641,12 @@ int reserve_zeroed(DevBuf& b, size_t bytes, hipStream_t stream)
 //   8 KiB     31.5    34.6    37.9    41.1     47.3     53.0     66.0
 //   16 KiB    43.0    43.8    46.5    46.1     48.1     53.1     63.6
 // so 8 KiB pieces from 112 MiB (128 MiB: 41.1 against 45.9) to 224 MiB.
+// And above (us per batch, 16 / 32 / 64 KiB pieces with the 4- or 2-row ring):
+//   batch     512 MiB          1 GiB            2 GiB            3 GiB
+//   16 KiB    107.9 / 112.7    191.2 / 198.6    366.3 / 366.3    551.4 / 543.0
+//   32 KiB    106.9 / 127.4    192.2 / 199.0    359.9 / 354.4    538.0 / 522.7
+//   64 KiB    124.8 / 181.1    196.6 / 237.8    354.9 / 374.6    534.0 / 517.9
+// so 32 KiB pieces with the 2-row ring from 1.5 GiB to 3 GiB.
 constexpr int kSortRingSmall = 4;
 
 uint32_t sorted_piece_log2(uint64_t total_bytes)
@@ -648,13 +654,14 @@ uint32_t sorted_piece_log2(uint64_t total_bytes)
     if (total_bytes < (uint64_t(32) << 20)) return 11;
     if (total_bytes < (uint64_t(112) << 20)) return 12;
     if (total_bytes < (uint64_t(224) << 20)) return 13;
-    if (total_bytes < (uint64_t(3) << 30)) return 14;
+    if (total_bytes < (uint64_t(3) << 29)) return 14;
+    if (total_bytes < (uint64_t(3) << 30)) return 15;
     return kSortPieceLog2;
 }
 
-// Rows in flight per wave in the sorted kernel's hash loop: 64 KiB pieces
-// (the full configs[2] batch, HBM-bound) take the 2-row ring, smaller pieces
-// (batches below 3 GiB, where a wave has a group or two) a deeper one.
+// Rows in flight per wave in the sorted kernel's hash loop: 32 and 64 KiB
+// pieces (batches from 1.5 GiB, the full configs[2] batch; HBM-bound) take
+// the 2-row ring, smaller pieces (where a wave has a group or two) a deeper one.
 // MI_CRC32C_SORT_RING=2|4 overrides (A/B, tests).
 int sorted_ring(uint32_t plog)
 {
@@ -663,7 +670,7 @@ int sorted_ring(uint32_t plog)
         const int r = std::atoi(e);
         if (r == 2 || r == 4) return r;
     }
-    return plog < kSortPieceLog2 ? kSortRingSmall : 2;
+    return plog < 15 ? kSortRingSmall : 2;
 }
 
 // Records spanning at most this many 128-B rows are hashed one per lane

@@ -98,7 +98,7 @@ def test_fuzz_round(engine, oracle, round_):
     # piece), one workgroup per CU or a few workgroups (shares cut inside
     # records), at a random piece size (512 B - 64 KiB)
     grid = [None, "1", "2", "5", "64"][int(rng.integers(0, 5))]
-    plog = [None, "9", "10", "12", "13", "14", "16"][int(rng.integers(0, 7))]
+    plog = [None, "9", "10", "12", "13", "14", "15", "16"][int(rng.integers(0, 8))]
     ring = [None, "2", "4"][int(rng.integers(0, 3))]
     lanes = [None, "0", "1", "3"][int(rng.integers(0, 4))]  # rows of a lane item (default 2)
     os.environ["MI_CRC32C_VARPATH"] = "sorted"

@@ -2,8 +2,8 @@
 one team per whole record, records binned by row count inside each
 workgroup's cost-balanced share, split records XORed together from their
 pieces.  The piece is sized by the batch (engine.hip sorted_piece_log2: 2 KiB
-below 32 MiB, 4 KiB below 112 MiB, 8 KiB below 224 MiB, 16 KiB below 3 GiB,
-64 KiB above); every
+below 32 MiB, 4 KiB below 112 MiB, 8 KiB below 224 MiB, 16 KiB below 1.5 GiB,
+32 KiB below 3 GiB, 64 KiB above); every
 test runs with the size's own
 piece ("auto", 4-row ring, whole records finished in the loop), with the
 2-row ring (the finish pass), and with 64 KiB pieces forced
