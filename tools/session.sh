@@ -123,6 +123,13 @@ while [ $# -gt 0 ]; do
     piecesweep) for rnd in 1 2; do for pl in ${SWEEP_PLOG:-13 14 15 16}; do for rg in ${SWEEP_RING:-4 2}; do
                MI_CRC32C_SORT_PIECE_LOG2=$pl MI_CRC32C_SORT_RING=$rg timeout -k 10 120 python3 tools/mid_probe.py --path sorted --mib ${MID_MIB:-128,256,512} --reps 100 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd plog=$pl ring=$rg /"
              done; done; done | tee "$OUT/piecesweep.out" ;;
+    zipfenv) for rnd in 1 2 3 4; do for e in ${ZENV:-NONE=1}; do
+               r=$(env ${e//,/ } timeout -k 10 120 python3 tools/zipf_probe.py consus_amd/lib/libconsus_crc32c.so 2>&1 | tail -1) || { echo "$r"; exit 1; }
+               echo "round $rnd $e $r"; case "$r" in *MISMATCH*) exit 1;; esac
+             done; done | tee "$OUT/zipfenv.out" ;;
+    midenv) for rnd in 1 2; do for e in ${MENV:-NONE=1}; do
+               env ${e//,/ } timeout -k 10 120 python3 tools/mid_probe.py --mib ${MID_MIB:-64,128,256} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd $e /"
+             done; done | tee "$OUT/midenv.out" ;;
     adaptab) for rnd in 1 2 3 4; do for cfg in ${ADAPT_SET:-head:1 head:0}; do
                v=${cfg%%:*}; a=${cfg##*:}; lib=tools/ab/libconsus_crc32c_$v.so; [ "$v" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
                r=$(MI_CRC32C_SORT_ADAPT=$a timeout -k 10 120 python3 tools/zipf_probe.py $lib 2>&1 | tail -1) || { echo "$r"; exit 1; }
