@@ -811,7 +811,7 @@ def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
     return res
 
 
-def run_mid(E, sizes_mib=(1, 4, 16, 20, 64, 256), reps: int = 200) -> dict:
+def run_mid(E, sizes_mib=(1, 4, 16, 20, 64, 128, 256), reps: int = 200) -> dict:
     """Mid-size device batches (VERDICT r4 Next 4; a durable-log segment,
     /root/reference/txman/durable_log.cc:287-347): configs[2]'s record stream
     cut to N MiB, one batch per launch on the engine's own path choice (the
