@@ -4,6 +4,10 @@ record stream cut to N MiB, timed per batch on the chosen variable-length path
 back-to-back batches after a clock warm-up; checked against the oracle.
 
     python tools/mid_probe.py [--mib 16,64,256] [--reps 200] [--path pieces|sorted|mid]
+                              [--uniform LO,HI]
+
+--uniform LO,HI replaces the configs[2] lengths with uniform LO..HI-byte
+records packed back to back (durable-log-like entries: 42,1024).
 """
 import os
 import sys
@@ -30,6 +34,11 @@ if PATH:
 
 E.init(0)
 off_all, ln_all, _ = W.zipf_records(1 << 20)
+if "--uniform" in sys.argv:
+    lo, hi = (int(x) for x in arg("--uniform", "42,1024").split(","))
+    ln_all = np.random.default_rng(7).integers(lo, hi + 1, ln_all.size).astype(np.uint32)
+    off_all = np.zeros(ln_all.size, dtype=np.uint64)
+    off_all[1:] = np.cumsum(ln_all[:-1], dtype=np.uint64)
 cum = np.cumsum(ln_all, dtype=np.uint64)
 data = E.DeviceBuffer(int(cum[-1]) + 16)
 data.fill_splitmix64(W.DATA_SEED)

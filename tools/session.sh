@@ -130,6 +130,10 @@ while [ $# -gt 0 ]; do
     midenv) for rnd in 1 2; do for e in ${MENV:-NONE=1}; do
                env ${e//,/ } timeout -k 10 120 python3 tools/mid_probe.py --mib ${MID_MIB:-64,128,256} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd $e /"
              done; done | tee "$OUT/midenv.out" ;;
+    smallrec) for rnd in 1 2; do for cfg in ${SMALLREC_CFGS:-engine_0_0 window_0_0 window_768_4 window_256_4 sorted_0_0}; do
+               set -- ${cfg//_/ }; p=$1; [ "$p" = engine ] && p=""
+               env MI_CRC32C_WIN_MAX_COUNT=16384 $( [ "$2" != 0 ] && echo MI_CRC32C_WIN_BLOCK=$2 ) $( [ "$3" != 0 ] && echo MI_CRC32C_WIN_ROWS=$3 ) timeout -k 10 120 python3 tools/mid_probe.py ${p:+--path $p} --uniform 42,1024 --mib ${MID_MIB:-1,2,4,6,8} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd $cfg /"
+             done; done | tee "$OUT/smallrec.out" ;;
     adaptab) for rnd in 1 2 3 4; do for cfg in ${ADAPT_SET:-head:1 head:0}; do
                v=${cfg%%:*}; a=${cfg##*:}; lib=tools/ab/libconsus_crc32c_$v.so; [ "$v" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
                r=$(MI_CRC32C_SORT_ADAPT=$a timeout -k 10 120 python3 tools/zipf_probe.py $lib 2>&1 | tail -1) || { echo "$r"; exit 1; }
