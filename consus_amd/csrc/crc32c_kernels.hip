@@ -3260,31 +3260,33 @@ uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, in
 // ---------------------------------------------------------------------------
 // Window path (round 5, VERDICT r4 Next 4): mid-size device batches in ONE
 // launch, no cost kernel, no LDS table image.  A record [a, E) covers the
-// 128-B rows [Rs, Re); it is cut into windows of kWinRows rows counted back
-// from its end: window k = rows [Re - 16 (k + 1), Re - 16 k) within [Rs, Re)
-// (K = ceil((L + 127) / 2048) windows: an upper bound taken from the length
-// alone, so the last may be empty).  A team (8 lanes) hashes one window: its
-// 16 rows are issued at once (16 dwordx4 per lane in flight) and folded
-// through the lane tables (ds_bpermute; the sorted kernel's 152 KiB LDS image
-// took 3.7 us to stage on a 1 MiB batch) as four independent chains of 4 rows,
-// joined with Z_512 and Z_1024 (a 16-row chain measured 3.8 us of a 1 MiB
-// batch's 13.1, profiles/r05_window_parts.txt).  The team's fold value W is the
-// raw state of the window's bytes as of row Re - 16 k; Z_{2048 k}(W) (one L2
-// table) moves it to row Re.  ~init rides in the record's first four bytes
-// (the sorted kernel's init word; a record of < 4 bytes takes the seed
-// Z_L(~init) instead).  The windows of a record that fall in one wave are
-// XORed there (team leaders' values through 16 permutes); a record within
-// one wave is finished by its first team: crc = ~Z_{-m}(XOR), m = 128 Re - E.
-// A record over several waves (segments) XORs each segment's value into the
-// low half of a 64-bit word acc[r] and its segment bit into the high half in
-// ONE atomic; the segment that completes the mask finishes the record and
-// zeroes the word (three dependent device-scope atomics per window measured
-// 1.8 / 4.8 / 17 us of a 1 / 4 / 16 MiB batch).  Records of more than 32
-// segments take the acc32 / cnt form (XOR, acq_rel count, swap).  All
-// workspace words are zero between launches.  Tasks (r, window) are numbered
-// by a prefix over the record lengths that every workgroup computes for
-// itself in LDS (count <= kWinMaxCount): no second launch, no grid barrier.
-// A grid smaller than the task count (understated total) loops; it never fails.
+// 128-B rows [Rs, Re); it is cut into windows of R rows (R = 4, 8 or 16)
+// counted back from its end: window k = rows [Re - R (k + 1), Re - R k) within
+// [Rs, Re) (K = ceil((L + 127) / 128 R) windows: an upper bound taken from the
+// length alone, so the last may be empty).  A team (8 lanes) hashes one
+// window: its R rows are issued at once (R dwordx4 per lane in flight) and
+// folded through the lane tables (ds_bpermute; the sorted kernel's 152 KiB LDS
+// image took 3.7 us to stage on a 1 MiB batch) as independent chains of 4
+// rows, joined with Z_512 and Z_1024 (a 16-row chain measured 3.8 us of a
+// 1 MiB batch's 13.1, profiles/r05_window_parts.txt).  The team's fold value W
+// is the raw state of the window's bytes as of row Re - R k; Z_{128 R k}(W)
+// (the Z_{512 j} L2 table, zshift48 past it) moves it to row Re.  ~init rides
+// in the record's first four bytes (the sorted kernel's init word; a record
+// of < 4 bytes takes the seed Z_L(~init) instead).  The windows of a record
+// that fall in one wave are XORed there (team leaders' values through 16
+// permutes); a record within one wave is finished by its first team:
+// crc = ~Z_{-m}(XOR), m = 128 Re - E.  A record over several waves (segments)
+// XORs each segment's value into the low half of a 64-bit word acc64[r] and
+// its segment bit into the high half in ONE atomic; the segment that
+// completes the mask finishes the record and zeroes the word (three dependent
+// device-scope atomics per window measured 1.8 / 4.8 / 17 us of a 1 / 4 /
+// 16 MiB batch).  Records of more than 32 segments take the acc / cnt form
+// (XOR, acq_rel count, swap).  All workspace words are zero between launches.
+// Tasks (r, window) are numbered by a prefix over the record lengths that
+// every workgroup computes for itself in LDS (count <= kWinMaxCountBig): no
+// second launch, no grid barrier.  Workgroups of 64, 256 or 768 threads
+// (launch_window's rule; 768: one per CU, looping).  A grid smaller than the
+// task count (understated total) loops; it never fails.
 // ---------------------------------------------------------------------------
 #ifndef MI_WIN_SKIP
 #define MI_WIN_SKIP 0  // A/B timing builds only (wrong CRCs): 1 no combine, 2 no lookups, 4 no fold
@@ -3302,8 +3304,7 @@ __device__ __forceinline__ uint32_t win_count(uint32_t L)
     return (L + kRowBytes - 1 + R * kRowBytes - 1) / (R * kRowBytes);
 }
 
-// B threads per workgroup, R rows per window (16, or 8 for batches that have
-// fewer windows than the chip has CUs: twice the waves, half the permutes each)
+// B threads per workgroup (64, 256, kWinBlockBig), R rows per window (4, 8, 16)
 template <uint32_t B, uint32_t R>
 __global__ __launch_bounds__(B) void crc32c_window_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
