@@ -750,7 +750,7 @@ int run_window(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     if ((st = reserve_zeroed(c->win_acc, count * 16, c->stream))) return st;
     uint64_t* acc64 = c->win_acc.as<uint64_t>();
     uint32_t* acc = reinterpret_cast<uint32_t*>(acc64 + count);
-    // MI_CRC32C_WIN_BLOCK=64|256, MI_CRC32C_WIN_ROWS=4|8|16: the workgroup and
+    // MI_CRC32C_WIN_BLOCK=64|256|768, MI_CRC32C_WIN_ROWS=4|8|16: the workgroup and
     // the window (A/B, tests; default by count and size)
     uint32_t block = 0, rows = 0;
     if (const char* e = std::getenv("MI_CRC32C_WIN_BLOCK")) block = std::atoi(e) == 64 ? 64u : std::atoi(e) == int(kWinBlockBig) ? kWinBlockBig : 256u;
