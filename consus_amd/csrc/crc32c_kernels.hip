@@ -3323,7 +3323,10 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
     __syncthreads();
     // (2) exclusive prefix: a contiguous run of records per thread
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t per = (count + B - 1) / B;
+    // an odd run length: the runs of a wave's lanes start in distinct LDS banks
+    // (a run of 16 made every read a 32-way conflict: 11,822 records in
+    // 768-thread workgroups took 6-7 us more, profiles/r05_window_small_records.txt)
+    const uint32_t per = ((count + B - 1) / B) | 1u;
     const uint32_t i0 = min(count, threadIdx.x * per), i1 = min(count, i0 + per);
     uint32_t own = 0;
     for (uint32_t i = i0; i < i1; ++i) own += s_pre[i];
