@@ -389,12 +389,12 @@ def cpu_baseline(args) -> dict:
             "slicing_by_8_single_thread_value": round(sb8, 2),
             "thread_sweep_gib_s": sweep,
             "host": cpus,
-            "sample": f"first {n} of the same {L}-B records ({n * L >> 20} MiB, host DRAM), "
-                      f"consus::crc32c from common/crc32c.cc compiled unmodified "
-                      f"(dispatch {'sse42 crc32q' if ref.lib.ref_dispatch_is_sse42() else 'slicing-by-8'}), "
-                      f"{pm} passes x {usable} std::threads (= min(affinity {cpus['affinity']}, "
-                      f"cgroup quota {cpus['cgroup_quota_cpus']}); nproc {cpus['nproc']}), "
-                      f"cpu: {cpus['model']}",
+            "sample": f"first {n} x {L} B of the same records ({n * L >> 20} MiB, host DRAM); "
+                      f"common/crc32c.cc compiled unmodified, "
+                      f"{'sse42 crc32q' if ref.lib.ref_dispatch_is_sse42() else 'slicing-by-8'}; "
+                      f"{pm} passes x {usable} std::threads = min(affinity {cpus['affinity']}, "
+                      f"cgroup quota {cpus['cgroup_quota_cpus']}), nproc {cpus['nproc']}; "
+                      f"{cpus['model']}",
             "first_crc": int(crc_ref[0])}
 
 
@@ -450,13 +450,14 @@ def run_dlog(args, compact: bool = False) -> dict:
         w["per"] = max(100, int(w["per"] * scale))
     runs = {w: {e: [] for e, _ in engines} for w, _ in workloads}
     try:
-        for _ in range(nruns):
+        for i in range(nruns):
             for wname, w in workloads:
+                if i == 0:  # one progress line per workload (the runs are interleaved)
+                    progress(f"durable log: {wname}, {nruns} interleaved runs x {len(engines)} engines")
                 for name, extra in engines:
                     env = dict(os.environ)
                     env.update(w["env"])
                     env.update(extra)
-                    progress(f"durable log run: {wname} / {name}")
                     r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(w["per"]),
                                         str(w["lo"]), str(w["hi"])],
                                        capture_output=True, text=True, timeout=300, env=env)
@@ -856,7 +857,7 @@ def run_mid(E, sizes_mib=(1, 4, 16, 20, 64, 128, 256), reps: int = 200) -> dict:
         for b in (data, d_off, d_len, out):
             b.free()
     return {"unit": "us per device batch", "reps": reps,
-            "workload": "configs[2] records (Zipf 64 B - 64 KiB) cut to N MiB, device-resident",
+            "workload": "configs[2] records cut to N MiB, device-resident",
             "batches": rows}
 
 
@@ -1012,6 +1013,130 @@ def run_zipf_sharded(args, E, dist, rank, world):
             "ranks": ranks, "distinct_gpus": len({r["pci_bus_id"] for r in ranks}),
             "cpu_baseline": None}), flush=True)
     dist.destroy_process_group()
+
+
+# ---- the default line, compacted (VERDICT r5 Next 1) ----------------------------
+# The driver keeps about the last 11.5 KB of the run's output: the whole
+# default line must fit well inside it, with configs[2]'s leg last.  The full
+# record (per-run arrays, long sample strings, host details) goes to a
+# detail file that the line names.
+LINE_LIMIT = 6000
+# legs in the line's order: the driver's record ends with configs[4] and configs[2]
+LEG_ORDER = ("mid_batches", "durable_log", "config1_pcie_inclusive", "config4_stream",
+             "config2_zipf")
+
+
+def _pick(d: dict | None, keys) -> dict | None:
+    if d is None:
+        return None
+    return {k: d[k] for k in keys if k in d}
+
+
+def _compact_cpu(c: dict | None, sample_chars: int = 120) -> dict | None:
+    if not c:
+        return c
+    r = _pick(c, ("value", "unit", "cores", "kind", "single_thread_value", "matches_gpu", "error"))
+    if "sample" in c:
+        # the sample's first clause (what was hashed); the rest is in the detail file
+        s = c["sample"].split(", consus::crc32c")[0].split("; ")[0]
+        r["sample"] = s if len(s) <= sample_chars else s[:sample_chars - 3] + "..."
+    return r
+
+
+def _compact_secondary(r: dict) -> dict:
+    """configs[2], configs[4] and the PCIe-inclusive leg: value, step time,
+    roofline, digest check and the same-run reference CPU rate."""
+    if "error" in r and "value" not in r:
+        return r
+    out = _pick(r, ("metric", "value", "unit", "ms_per_step", "steps", "warmup"))
+    out["workload"] = (r.get("config") or {}).get("workload")
+    out["roofline"] = _pick(r.get("roofline"), ("bound", "achieved", "peak", "frac", "traffic",
+                                                "algorithmic_bytes", "step_ms_events"))
+    out["digest_verified"] = r.get("digest_verified")
+    if r.get("sustained"):
+        out["sustained"] = _pick(r["sustained"], ("steps", "step_ms", "frac", "digest_unchanged"))
+    out["cpu_baseline"] = _compact_cpu(r.get("cpu_baseline"), 90)
+    out["leg_wall_s"] = r.get("leg_wall_s")
+    return out
+
+
+def _compact_mid(r: dict) -> dict:
+    if "batches" not in r:
+        return r
+    return {"unit": r.get("unit"), "reps": r.get("reps"), "workload": r.get("workload"),
+            "cols": ["mib", "us_per_batch", "gb_s", "path", "crc_ok"],
+            "batches": [[b["mib"], b["us_per_batch"], b["gb_s"], b["path"], b["crc_ok"]]
+                        for b in r["batches"]],
+            "leg_wall_s": r.get("leg_wall_s")}
+
+
+def _compact_dlog(r: dict) -> dict:
+    """Per workload and engine: appends/s median, q1, q3 and the medians of the
+    runs' p50 / p99 durable latency; the GPU engine against each other engine;
+    the median GPU run's per-flush phases."""
+    if "workloads" not in r:
+        return r
+    out = _pick(r, ("value", "unit", "steps", "digest_verified"))
+    out["metric"] = "durable-log appends/s, 8 appending threads"
+    out["cols"] = "appends/s median q1 q3, durable-latency us p50 p99"
+    for wname, w in r["workloads"].items():
+        e = {name: [round(s["appends_per_s"][q]) for q in ("median", "q1", "q3")] +
+             [round(s["durable_latency_us"][q]) for q in ("p50_median", "p99_median")]
+             for name, s in w["engines"].items()}
+        f = w.get("flush", {})
+        out[wname] = {
+            "engines": e,
+            "gpu_vs": {k: [v["appends_ratio"], v["beyond_spread"].replace(" run spread", "")]
+                       for k, v in w.get("gpu_vs", {}).items()},
+            "flush": dict(_pick(f, ("flushes", "host_flushes", "frame_bytes_per_flush",
+                                    "batch_crc_vs_bound")),
+                          us_per_flush=_pick(f.get("us_per_flush", {}),
+                                             ("walk", "batch_crc", "patch", "pwrite")))}
+    out["cpu_baseline"] = _compact_cpu(r.get("cpu_baseline"), 100)
+    if out["cpu_baseline"]:
+        out["cpu_baseline"]["sample"] = "engine reference-scheme, uniform workload"
+    out["leg_wall_s"] = r.get("leg_wall_s")
+    return out
+
+
+def compact_line(rec: dict, detail: str | None) -> dict:
+    """The default line as printed: the headline keys unchanged, the legs
+    compacted and in LEG_ORDER (configs[2] last), `detail_file` naming the
+    full record."""
+    line = {k: v for k, v in rec.items() if k not in LEG_ORDER}
+    if line.get("cpu_baseline"):
+        c = dict(line["cpu_baseline"])
+        c.pop("host", None)  # in the detail file; the sample names the CPU model
+        c.pop("first_crc", None)
+        line["cpu_baseline"] = c
+    if detail:
+        line["detail_file"] = detail
+    for k in LEG_ORDER:
+        if k not in rec:
+            continue
+        r = rec[k]
+        if k == "mid_batches":
+            line[k] = _compact_mid(r)
+        elif k == "durable_log":
+            line[k] = _compact_dlog(r)
+        else:
+            line[k] = _compact_secondary(r)
+    return line
+
+
+def write_detail(rec: dict) -> str | None:
+    """The full record (every run, every sample string) to BENCH_DETAIL, by
+    default gpurun_out/bench_detail.json; returns the path the line names."""
+    path = os.environ.get("BENCH_DETAIL", os.path.join(REPO, "gpurun_out", "bench_detail.json"))
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(rec, f)
+            f.write("\n")
+    except OSError as e:
+        progress(f"detail file not written: {e}")
+        return None
+    return os.path.relpath(path, REPO) if os.path.abspath(path).startswith(REPO) else path
 
 
 def main():
@@ -1252,6 +1377,8 @@ def main():
         multi_rank_fields(rec, ranks, None, world, args.share_device)
         gather = rccl_gather(E, dist, rank, world, out, R, digests, rec) if do_gather else None
         code = multi_rank_fields(rec, ranks, gather, world, args.share_device)
+    if leg_res:
+        rec = compact_line(rec, write_detail(rec))
     print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()
