@@ -165,7 +165,10 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
 // Window path (launch_window): mid-size batches of at most kWinMaxCount
 // records in one launch; each record cut into windows of 4, 8 or 16 rows from
 // its end, one per team.  acc64 / acc / cnt: count words each, zero before
-// and after.
+// and after.  ctrl: the sorted path's control words; ctrl[1] = 1 (and the
+// sticky ctrl[2]) when the batch numbers more than 2^31 windows, which only
+// a total_bytes hint understated by a factor ~80,000 lets through (nothing
+// is hashed then; the engine recovers as for the sorted path's overflow).
 constexpr uint32_t kWinBlockMax = 256;   // workgroup of batches above kWinSmallCount records
 constexpr uint32_t kWinSmallCount = 768;  // ... and one wave per workgroup up to it
 constexpr uint32_t kWinMaxCount = 8192;     // the engine's record bound (MI_CRC32C_WIN_MAX_COUNT: probes)
@@ -176,7 +179,7 @@ uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_
 hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
                          uint64_t* acc64, uint32_t* acc, uint32_t* cnt, const uint32_t* tables,
-                         const uint32_t* pow2, int grid_cap,
+                         const uint32_t* pow2, uint32_t* ctrl, int grid_cap,
                          uint32_t block,  // 0: by count; 64, 256
                          uint32_t rows,   // rows per window, 0: by size; 4, 8, 16
                          hipStream_t stream);

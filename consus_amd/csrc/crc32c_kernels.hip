@@ -3298,11 +3298,21 @@ __device__ __forceinline__ uint32_t wave_min32(uint32_t x)
     return x;
 }
 
+// Windows of a record of L bytes, computed in 64 bits: a record of close to
+// 4 GiB wrapped the 32-bit sum to 0 windows.
 template <uint32_t R>
 __device__ __forceinline__ uint32_t win_count(uint32_t L)
 {
-    return (L + kRowBytes - 1 + R * kRowBytes - 1) / (R * kRowBytes);
+    return uint32_t((uint64_t(L) + kRowBytes - 1 + R * kRowBytes - 1) / (R * kRowBytes));
 }
+// Tasks a launch may number: task indices, the round cursor and the records'
+// first tasks stay in 32 bits below it.  A batch with more (only with a
+// total_bytes hint understated ~80,000-fold: 2^31 windows are >= 1 TiB of
+// records) stores ctrl[1] = ctrl[2] = 1 and hashes nothing, as the sorted
+// path does when its workspace overflows: the engine recomputes a
+// synchronous batch on the plan path and reports an asynchronous one at the
+// next stream sync.
+constexpr uint64_t kWinMaxTasks = uint64_t(1) << 31;
 
 // B threads per workgroup (64, 256, kWinBlockBig), R rows per window (4, 8, 16)
 template <uint32_t B, uint32_t R>
@@ -3310,11 +3320,12 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ inits, uint32_t count,
     uint32_t* __restrict__ out, uint64_t* __restrict__ acc64, uint32_t* __restrict__ acc,
-    uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2)
+    uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2,
+    uint32_t* __restrict__ ctrl)
 {
-    // LDS: first task of each record, wave sums
+    // LDS: first task of each record, wave sums (64-bit, 8-B aligned)
     uint32_t* const s_pre = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* const s_wsum = s_pre + count;
+    uint64_t* const s_wsum = reinterpret_cast<uint64_t*>(smem + ((size_t(count) * 4 + 7) & ~size_t(7)));
     LaneTabs lt;
     load_lane_tabs<6 * kLaneOps>(lt, tables);
     // (1) windows per record, from the lengths alone (an empty record: one
@@ -3328,25 +3339,31 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
     // 768-thread workgroups took 6-7 us more, profiles/r05_window_small_records.txt)
     const uint32_t per = ((count + B - 1) / B) | 1u;
     const uint32_t i0 = min(count, threadIdx.x * per), i1 = min(count, i0 + per);
-    uint32_t own = 0;
+    uint64_t own = 0;
     for (uint32_t i = i0; i < i1; ++i) own += s_pre[i];
-    uint32_t x = own;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1)
-    {
-        const uint32_t y = uint32_t(__shfl_up(int(x), d));
-        if (lane >= uint32_t(d)) x += y;
-    }
+    const uint64_t x = wave_incl_scan64(own);
     if (lane == 63) s_wsum[wave] = x;
     __syncthreads();
-    uint32_t run = x - own, ntask = 0;
+    uint64_t run64 = x - own, ntask64 = 0;
 #pragma unroll
     for (uint32_t w = 0; w < B / 64; ++w)
     {
-        const uint32_t s = s_wsum[w];
-        run += w < wave ? s : 0u;
-        ntask += s;
+        const uint64_t s = s_wsum[w];
+        run64 += w < wave ? s : 0u;
+        ntask64 += s;
     }
+    if (ntask64 > kWinMaxTasks)  // workgroup-uniform, and the same in every workgroup
+    {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+        {
+            ctrl[1] = 1;
+            ctrl[2] = 1;  // sticky: an asynchronous batch's is reported at the next stream sync
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctrl[1] = 0;
+    const uint32_t ntask = uint32_t(ntask64);
+    uint32_t run = uint32_t(run64);
     for (uint32_t i = i0; i < i1; ++i)
     {
         const uint32_t c = s_pre[i];
@@ -3518,7 +3535,7 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
     }
 }
 
-size_t window_lds_bytes(uint32_t count) { return size_t(count) * 4 + 4 * (kWinBlockBig / 64); }
+size_t window_lds_bytes(uint32_t count) { return ((size_t(count) * 4 + 7) & ~size_t(7)) + 8 * (kWinBlockBig / 64); }
 
 uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_t block, uint32_t rows)
 {
@@ -3531,8 +3548,8 @@ uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_
 hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,
                          uint64_t* acc64, uint32_t* acc, uint32_t* cnt, const uint32_t* tables,
-                         const uint32_t* pow2, int grid_cap, uint32_t block, uint32_t rows,
-                         hipStream_t stream)
+                         const uint32_t* pow2, uint32_t* ctrl, int grid_cap, uint32_t block,
+                         uint32_t rows, hipStream_t stream)
 {
     if (count == 0) return hipSuccess;
     if (count > kWinMaxCountBig) return hipErrorInvalidValue;
@@ -3571,7 +3588,7 @@ hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32
                                                     : crc32c_window_kernel<kWinBlockMax, 16>);
     hipLaunchKernelGGL(k, dim3(g), dim3(block), window_lds_bytes(uint32_t(count)), stream,
                        static_cast<const uint8_t*>(base), offsets, lengths, inits, uint32_t(count),
-                       out, acc64, acc, cnt, tables, pow2);
+                       out, acc64, acc, cnt, tables, pow2, ctrl);
     return hipGetLastError();
 }
 

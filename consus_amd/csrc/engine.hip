@@ -347,6 +347,10 @@ struct Ctx
     // an asynchronous sorted batch ran since the last stream sync: its
     // overflow (understated size hint) sits in the sticky ctrl[2]
     bool async_sorted_unchecked = false;
+    // the sticky word as earlier asynchronous batches left it, read
+    // before a synchronous batch ran on the stream (which may set and clear
+    // the word itself); reported by the next stream sync
+    bool async_overflow_latched = false;
     // the one-launch sorted form: this context counted in its device's
     // sorted_users, and the barrier counter's value before the next launch
     std::atomic<int>* sorted_users = nullptr;
@@ -538,8 +542,13 @@ const uint8_t* mapped_span_device_ptr(const uint8_t* p, uint64_t n)
     }
     (void)hipGetLastError();
     // no allocation range: every page between the two ends, mapped at the
-    // same distance
+    // same distance.  One runtime query per page, so the walk is capped
+    // (sparse records across a multi-GiB registered buffer cost
+    // hundreds of thousands of queries per batch); a longer span is staged
+    // by a CPU copy, which is correct, only slower.
     constexpr uint64_t kPage = 4096;
+    constexpr uint64_t kWalkMaxBytes = 2 * kDirectMaxBytes + (uint64_t(64) << 20);  // a 64 MiB segment
+    if (n > kWalkMaxBytes) return nullptr;
     const uintptr_t first = (reinterpret_cast<uintptr_t>(p) | (kPage - 1)) + 1;
     for (uintptr_t q = first; q < reinterpret_cast<uintptr_t>(p) + n; q += kPage)
     {
@@ -747,7 +756,9 @@ int run_window(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
 {
     int st;
-    if ((st = reserve_zeroed(c->win_acc, count * 16, c->stream))) return st;
+    if ((st = reserve_zeroed(c->win_acc, count * 16, c->stream)) ||
+        (st = reserve_zeroed(c->srt_ctrl, 64 * 4, c->stream)))
+        return st;
     uint64_t* acc64 = c->win_acc.as<uint64_t>();
     uint32_t* acc = reinterpret_cast<uint32_t*>(acc64 + count);
     // MI_CRC32C_WIN_BLOCK=64|256|768, MI_CRC32C_WIN_ROWS=4|8|16: the workgroup and
@@ -757,7 +768,14 @@ int run_window(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     if (const char* e = std::getenv("MI_CRC32C_WIN_ROWS"))
         rows = std::atoi(e) == 4 ? 4u : std::atoi(e) == 8 ? 8u : 16u;
     HIP_TRY(launch_window(base, off, len, inits, count, total_bytes, out, acc64, acc, acc + count,
-                          d->d_tables, d->d_pow2, 8 * d->cus, block, rows, c->stream));
+                          d->d_tables, d->d_pow2, c->srt_ctrl.as<uint32_t>(), 8 * d->cus, block, rows,
+                          c->stream));
+    // more than 2^31 windows (an understated hint) set ctrl[1] and
+    // the sticky ctrl[2]; the batch is then checked as a sorted batch is
+    // (a synchronous one recomputed on the plan path, an asynchronous one
+    // reported at the next stream sync)
+    c->sorted_ctrl = c->srt_ctrl.as<uint32_t>();
+    c->bar_tag = 0;
     mi_host::note_window_batch();
     return MI_CRC32C_OK;
 }
@@ -919,16 +937,22 @@ int mi_crc32c_stream_sync(void)
     Ctx* c = thread_ctx(&st);
     if (!c) return st;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->async_sorted_unchecked)
+    if (c->async_sorted_unchecked || c->async_overflow_latched)
     {
-        // an asynchronous sorted batch whose total_bytes hint
-        // understated its records left out[] incomplete (no access went out
-        // of bounds); the kernel's sticky word says so, read and cleared here
-        c->async_sorted_unchecked = false;
+        // an asynchronous sorted (or window) batch whose
+        // total_bytes hint understated its records left out[] incomplete (no
+        // access went out of bounds); the kernel's sticky word says so, read
+        // and cleared here (or latched by a synchronous batch since)
         uint32_t* w = c->pin_small.as<uint32_t>() + 2;
-        HIP_TRY(hipMemcpyAsync(w, c->srt_ctrl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (*w)
+        *w = 0;
+        if (c->async_sorted_unchecked)
+        {
+            HIP_TRY(hipMemcpyAsync(w, c->srt_ctrl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
+        const bool latched = c->async_overflow_latched;
+        c->async_sorted_unchecked = c->async_overflow_latched = false;
+        if (*w || latched)
         {
             HIP_TRY(hipMemsetAsync(c->srt_ctrl.as<uint32_t>() + 2, 0, 4, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
@@ -988,12 +1012,31 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
     if (!c) return st;
     if (flags & MI_CRC32C_DEVICE)
     {
+        // before a synchronous batch, the sticky word as the
+        // unchecked asynchronous batches left it (pin_small word 8), latched
+        // once this batch's sync has read it; the word is then free for this
+        // batch's own overflow, which is recovered here
+        const bool pre = !(flags & MI_CRC32C_ASYNC) && c->async_sorted_unchecked;
+        uint32_t* pre_w = c->pin_small.as<uint32_t>() + 8;
+        if (pre)
+            HIP_TRY(hipMemcpyAsync(pre_w, c->srt_ctrl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost,
+                                   c->stream));
+        auto latch = [&]() {
+            if (!pre) return MI_CRC32C_OK;
+            c->async_overflow_latched |= *pre_w != 0;
+            c->async_sorted_unchecked = false;
+            HIP_TRY(hipMemsetAsync(c->srt_ctrl.as<uint32_t>() + 2, 0, 4, c->stream));
+            return MI_CRC32C_OK;
+        };
         c->sorted_ctrl = c->plan_total = nullptr;
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out)))
             return st;
         if (flags & MI_CRC32C_ASYNC) c->async_sorted_unchecked |= c->sorted_ctrl != nullptr;
         if ((flags & MI_CRC32C_ASYNC) || (!c->sorted_ctrl && !c->plan_total))
-            return finish(c, flags);
+        {
+            if ((st = finish(c, flags))) return st;
+            return latch();
+        }
         // Synchronous batch sized by the caller's hint: if the hint understated
         // the sum of lengths, the workspace overflowed and out[] is incomplete
         // (sorted path: a workgroup found no room for its descriptors; piece
@@ -1003,10 +1046,13 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         HIP_TRY(hipMemcpyAsync(flag, c->sorted_ctrl ? c->sorted_ctrl : c->plan_total,
                                c->sorted_ctrl ? 16 : 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((st = latch())) return st;
         // the one-launch form's barrier timed out (ctrl[3] holds this launch's
         // tag, bar_base after it + 1): hash the batch again with two launches
         if (c->sorted_ctrl && c->bar_tag && flag[3] == c->bar_tag)
         {
+            // ctrl[3], and this batch's sticky ctrl[2] (an unchecked
+            // asynchronous batch's state was latched above)
             HIP_TRY(hipMemsetAsync(c->sorted_ctrl + 2, 0, 8, c->stream));
             c->force_unfused = true;
             if ((st = run_var(d, c, base, offsets, lengths, inits, count, total_bytes, out))) return st;
@@ -1017,11 +1063,9 @@ int batch(int dev, const void* base, const uint64_t* offsets, const uint32_t* le
         const bool overflow = c->sorted_ctrl ? flag[1] != 0 : flag[0] > c->plan_cap;
         if (!overflow) return MI_CRC32C_OK;
         // the sticky word (ctrl[2]) is for asynchronous batches: this one is
-        // recovered here.  With an unchecked asynchronous batch before it on
-        // the stream the word may be that batch's too, so it stays for the
-        // next stream sync to report (conservatively).
-        if (c->sorted_ctrl && !c->async_sorted_unchecked)
-            HIP_TRY(hipMemsetAsync(c->sorted_ctrl + 2, 0, 4, c->stream));
+        // recovered here.  The earlier asynchronous batches' state was latched
+        // before this batch ran, so the word is cleared.
+        if (c->sorted_ctrl) HIP_TRY(hipMemsetAsync(c->sorted_ctrl + 2, 0, 4, c->stream));
         if ((st = run_var(d, c, base, offsets, lengths, inits, count, 0, out))) return st;
         return finish(c, flags);
     }

@@ -211,3 +211,141 @@ def test_understated_hint_on_an_async_batch_fails_the_next_sync(engine, oracle):
     assert np.array_equal(d_out.download(np.uint32, count), want)
     for b in (data, d_off, d_len, d_out):
         b.free()
+
+
+def _in_thread(fn):
+    """Run fn in a fresh thread (its own engine context); re-raise its error."""
+    import threading
+    box = {}
+
+    def run():
+        try:
+            box["v"] = fn()
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            box["e"] = e
+    t = threading.Thread(target=run)
+    t.start()
+    t.join()
+    if "e" in box:
+        raise box["e"]
+    return box.get("v")
+
+
+def _split_batch(engine, seed):
+    count = 64
+    lengths = np.full(count, 1 << 20, dtype=np.uint32)
+    offsets = (np.arange(count, dtype=np.uint64) << np.uint64(20)) + np.uint64(5)
+    size = (count << 20) + 4096
+    buf = np.random.default_rng(seed).integers(0, 256, size, dtype=np.uint8)
+    data = engine.DeviceBuffer(size)
+    data.upload(buf)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(offsets)
+    d_len.upload(lengths)
+    return count, buf, offsets, lengths, (data, d_off, d_len, d_out)
+
+
+@pytest.mark.parametrize("async_hint_ok", [True, False])
+def test_async_state_survives_a_recovered_sync_batch(engine, oracle, async_hint_ok):
+    """an unchecked asynchronous sorted batch, then a synchronous
+    sorted batch whose understated hint overflows and is recomputed.  The
+    next stream sync reports exactly the asynchronous batch's state: clean
+    when its hint was true (round 5 reported a false EINVAL: the sync batch
+    left the sticky word set), EINVAL when it was understated (the word as
+    the asynchronous batch left it is read before the synchronous batch
+    runs).  The synchronous batch's results are exact either way."""
+    count, buf, offsets, lengths, (data, d_off, d_len, d_out) = _split_batch(engine, 5)
+    want = oracle.batch(buf, offsets, lengths)
+    d_out2 = engine.DeviceBuffer(count * 4)
+
+    def run():
+        os.environ["MI_CRC32C_VARPATH"] = "sorted"
+        try:
+            engine.device_batch(data, d_off, d_len, count, d_out2,
+                                total_bytes=int(lengths.sum()) if async_hint_ok else 4 << 20,
+                                asynchronous=True)
+            engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=4 << 20)
+            got = d_out.download(np.uint32, count)
+            try:
+                engine.sync()
+                first = "ok"
+            except engine.EngineError as e:
+                first = e.status
+            engine.sync()
+            return got, first
+        finally:
+            os.environ.pop("MI_CRC32C_VARPATH", None)
+    got, first = _in_thread(run)
+    assert np.array_equal(got, want)
+    assert first == ("ok" if async_hint_ok else engine.EINVAL)
+    if async_hint_ok:
+        assert np.array_equal(d_out2.download(np.uint32, count), want)
+    for b in (data, d_off, d_len, d_out, d_out2):
+        b.free()
+
+
+def test_window_record_of_4gib_minus_one(engine, oracle):
+    """the window path counted a record's windows in 32 bits, so a
+    record of 0xFFFFFFFF bytes wrapped to no window and its CRC was never
+    stored.  One such record (bytes [1, 2^32) of the splitmix64 stream
+    0xC0DE), forced onto the window path, against the oracle over the same
+    bytes."""
+    n = 0xFFFFFFFF
+    data = engine.DeviceBuffer((1 << 32) + 64)
+    data.fill_splitmix64(0xC0DE)
+    d_off, d_len, d_out = engine.DeviceBuffer(8), engine.DeviceBuffer(4), engine.DeviceBuffer(4)
+    d_off.upload(np.array([1], dtype=np.uint64))
+    d_len.upload(np.array([n], dtype=np.uint32))
+    d_out.upload(np.array([0xABABABAB], dtype=np.uint32))
+    before = engine.stats()["window_batches"]
+    os.environ["MI_CRC32C_VARPATH"] = "window"
+    try:
+        engine.device_batch(data, d_off, d_len, 1, d_out, total_bytes=n)
+    finally:
+        os.environ.pop("MI_CRC32C_VARPATH", None)
+    assert engine.stats()["window_batches"] == before + 1
+    host = data.download(np.uint8, 1 << 32)
+    data.free()
+    want = oracle.crc32c(0, host[1:])
+    del host
+    assert int(d_out.download(np.uint32, 1)[0]) == want
+    for b in (d_off, d_len, d_out):
+        b.free()
+
+
+def test_window_task_overflow_on_an_async_batch_fails_the_next_sync(engine, oracle):
+    """1,100 aliased records of 0xFFFFFFFF bytes are 9.2e9 windows,
+    past the window path's 2^31 task bound, with a hint of 1 byte (which
+    routes them to the window path).  The kernel hashes nothing and sets the
+    sticky word; the next stream sync reports EINVAL (counted), and a true
+    batch after it on the same context is exact."""
+    count = 1100
+    data = engine.DeviceBuffer((1 << 32) + 64)
+    d_off, d_len, d_out = (engine.DeviceBuffer(count * 8), engine.DeviceBuffer(count * 4),
+                           engine.DeviceBuffer(count * 4))
+    d_off.upload(np.zeros(count, dtype=np.uint64))
+    d_len.upload(np.full(count, 0xFFFFFFFF, dtype=np.uint32))
+    rng = np.random.default_rng(9)
+    small = rng.integers(0, 256, 5000, dtype=np.uint8)
+
+    def run():
+        before = engine.stats()
+        engine.device_batch(data, d_off, d_len, count, d_out, total_bytes=1, asynchronous=True)
+        try:
+            engine.sync()
+            first = "ok"
+        except engine.EngineError as e:
+            first = e.status
+        after = engine.stats()
+        got = engine.crc32c_batch(small, np.array([0, 7], dtype=np.uint64),
+                                  np.array([4000, 900], dtype=np.uint32))
+        engine.sync()
+        return first, after["window_batches"] - before["window_batches"], \
+            after["hint_overflows"] - before["hint_overflows"], got
+    first, nwin, nover, got = _in_thread(run)
+    assert first == engine.EINVAL and nwin == 1 and nover == 1
+    assert np.array_equal(got, oracle.batch(small, np.array([0, 7], dtype=np.uint64),
+                                            np.array([4000, 900], dtype=np.uint32)))
+    for b in (data, d_off, d_len, d_out):
+        b.free()

@@ -5,7 +5,7 @@
 #   tools/session.sh tests route crossover rehearsal dlog zipf fixed ...
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$ROOT/gpurun_out/${SESSION:-r05}"
+OUT="$ROOT/gpurun_out/${SESSION:-r06}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT" || exit 9
@@ -56,6 +56,7 @@ while [ $# -gt 0 ]; do
     wskip) for rnd in 1 2; do for v in ${WSKIP_LIBS:-w0 wskip1 wskip2 wskip4 wskip3 wskip7}; do
              timeout -k 10 120 python3 tools/mid_probe.py --lib tools/ab/libconsus_crc32c_$v.so --path window --mib ${WIN_MIB:-1,4,16} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd /"
            done; done | tee "$OUT/wskip.out" ;;
+    errtests) run pytest_err 600 python -u -m pytest tests/test_gpu_errors.py tests/test_gpu_window.py -x -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
     flush) run flush_probe 300 ./tools/flush_probe 1000 ;;
