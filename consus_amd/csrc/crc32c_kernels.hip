@@ -2466,6 +2466,8 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
+// where each workgroup ran: HW_ID (cu, sh, se fields) and XCC_ID (round 6)
+__device__ uint32_t g_sort_hw[256 * 2];
 #define SORT_STAMP(k)                                                                        \
     do                                                                                       \
     {                                                                                        \
@@ -2511,6 +2513,13 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // has written the descriptor list out: until then their LDS holds the
     // list, so no table lookup may come before that call.)
     SORT_STAMP(0);
+#if MI_SORT_STAMP
+    if (threadIdx.x == 0 && blockIdx.x < 256)
+    {
+        g_sort_hw[2 * blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4);       // HW_REG_HW_ID
+        g_sort_hw[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    }
+#endif
     if (fused && !sorted_fused_costs(base, off, len, inits, count, blk_cost, nb, ctrl, out, tables,
                                      plog, bar_base, S))
         return;  // the grid barrier timed out: ctrl[3] tells the host (below)
@@ -3216,6 +3225,11 @@ extern "C" __attribute__((visibility("default"))) int mi_debug_sort_stamps(uint6
 {
     n = n < sizeof(g_sort_stamp) / 8 ? n : sizeof(g_sort_stamp) / 8;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_stamp), n * 8) == hipSuccess ? 0 : -5;
+}
+extern "C" __attribute__((visibility("default"))) int mi_debug_sort_hw(uint32_t* host, size_t n)
+{
+    n = n < sizeof(g_sort_hw) / 4 ? n : sizeof(g_sort_hw) / 4;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_hw), n * 4) == hipSuccess ? 0 : -5;
 }
 #endif
 

@@ -325,6 +325,7 @@ struct durable_log::write_job
     uint64_t file_off = 0;
     uint64_t upto = 0;    // watermark once written and synced
     uint64_t frames = 0;
+    size_t row = SIZE_MAX;  // flush_timeline row
     void release_ext()
     {
         for (segment::External& x : ext)
@@ -451,6 +452,34 @@ void durable_log::set_batch_crc_for_testing(durable_log_batch_crc fn, void* ctx)
     m_crc = fn ? fn : gpu_batch;
     m_crc_ctx = fn ? ctx : &m_opts;
     m_pinned = !fn;
+}
+
+void durable_log::set_pinned_arenas_for_testing(bool pinned)
+{
+    std::lock_guard<std::mutex> hold(m_mtx);
+    if (!m_opened) m_pinned = pinned;
+}
+
+// Rows of the flush timeline kept (a bench run flushes a few thousand times).
+constexpr size_t kTimelineRows = 1 << 14;
+
+double durable_log::since_open() const
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - m_t_open).count();
+}
+
+// Under m_mtx.
+void durable_log::mark(size_t row, int col, double v)
+{
+    if (row < m_timeline.size() / 7) m_timeline[row * 7 + size_t(col)] = v;
+}
+
+size_t durable_log::flush_timeline(double* out, size_t max_rows)
+{
+    std::lock_guard<std::mutex> hold(m_mtx);
+    const size_t n = std::min(max_rows, m_timeline.size() / 7);
+    std::copy(m_timeline.begin(), m_timeline.begin() + ptrdiff_t(n * 7), out);
+    return n;
 }
 
 void durable_log::set_append_crc_for_testing(uint32_t (*fn)(uint32_t, const unsigned char*, size_t))
@@ -626,6 +655,7 @@ bool durable_log::open(const std::string& dir)
     }
     m_segment_a = segs[0];
     m_segment_b = segs[1];
+    m_t_open = std::chrono::steady_clock::now();
     m_segment_a->base = 1;  // record numbers start at 1 (:151)
     m_segment_a->word.store(0);
     m_active.store(m_segment_a);
@@ -1043,9 +1073,11 @@ void durable_log::writer()
         if (m_jobs.empty()) return;  // m_stop_writer, nothing left to write
         write_job* job = m_jobs.front();
         m_jobs.erase(m_jobs.begin());
+        mark(job->row, 3, since_open());
         hold.unlock();
         const int e = m_error.load() > 0 ? 0 : write_out(job);
         hold.lock();
+        mark(job->row, 4, since_open());
         m_spare = job->arena;  // free again: the next sealed segment may take it
         m_spare_pinned = job->arena_pinned;
         job->arena = nullptr;
@@ -1056,7 +1088,7 @@ void durable_log::writer()
             m_cond.wait(hold, [&] { return (m_error != 0 && m_error != -1) || m_pending.empty(); });
             if (m_error == 0 || m_error == -1)
             {
-                m_pending.push_back(synced{job->fd, job->upto, job->frames});
+                m_pending.push_back(synced{job->fd, job->upto, job->frames, job->row});
                 m_cond.notify_all();
             }
         }
@@ -1095,6 +1127,7 @@ void durable_log::sync()
         else if (m_error == 0 || m_error == -1)
         {
             m_durable.store(job.upto);
+            mark(job.row, 5, since_open());
             ++m_flushes;
             m_frames_flushed += job.frames;
         }
@@ -1177,6 +1210,7 @@ void durable_log::flush()
         segment* seg = nullptr;
         uint64_t n = 0, used = 0;
         bool exact = true;
+        size_t row = SIZE_MAX;  // flush_timeline row of this flush
         {
             std::unique_lock<std::mutex> hold(m_mtx);
             m_flush_phase.store(1);
@@ -1208,6 +1242,12 @@ void durable_log::flush()
             used = w & kUsedMask;
             exact = used <= seg->cap && n <= seg->slots;
             if (exact) switch_to_next(seg, n);
+            if (m_timeline.size() / 7 < kTimelineRows)
+            {
+                row = m_timeline.size() / 7;
+                m_timeline.resize(m_timeline.size() + 7, 0.0);
+                mark(row, 0, since_open());
+            }
         }
         // every reservation taken before the seal finishes: its frame is
         // staged, or it did not fit (and its appender retries elsewhere)
@@ -1240,8 +1280,16 @@ void durable_log::flush()
         m_flush_phase.store(4);
         auto* job = new write_job;
         const int e = prepare_segment(seg, n, used, job);
+        const double t_prepared = since_open();
         {
             std::unique_lock<std::mutex> hold(m_mtx);
+            job->row = row;
+            mark(row, 1, t_prepared);
+            {
+                uint64_t bytes = job->used;
+                for (const segment::External& x : job->ext) bytes += x.bytes;
+                mark(row, 6, double(bytes));
+            }
             if (e)
             {
                 m_error = e;
@@ -1269,6 +1317,7 @@ void durable_log::flush()
             seg->pinned = m_spare_pinned;
             m_spare = nullptr;
             m_jobs.push_back(job);
+            mark(row, 2, since_open());
             m_cond.notify_all();
         }
     }

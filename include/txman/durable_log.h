@@ -37,6 +37,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <string>
@@ -128,6 +129,15 @@ class __attribute__((visibility("default"))) durable_log
         void set_external_malloc_failure_for_testing(bool fail);
         // Flushes checksummed on the flush thread's CPU (below host_batch_max).
         uint64_t host_flushes() const;
+        // Test hook (call before open): stage frames in pinned (true) or
+        // ordinary (false) memory whatever the batch engine (an injected
+        // engine defaults to ordinary memory, the GPU batch to pinned).
+        void set_pinned_arenas_for_testing(bool pinned);
+        // Bench hook: one row per flushed segment, up to max_rows, of 7
+        // values -- seconds since open() when it was sealed, checksummed
+        // (CRCs patched in), handed to the writer, written from, written to,
+        // synced, and its bytes.  Returns the rows written.
+        size_t flush_timeline(double* out, size_t max_rows);
         // One line of the log's internal state (flush-thread phase, the
         // active segment's reservation word, queued jobs, appenders waiting
         // for a switch) for watchdogs; writes at most n bytes, NUL included.
@@ -141,6 +151,7 @@ class __attribute__((visibility("default"))) durable_log
             int fd;
             uint64_t upto;                  // watermark once it is synced
             uint64_t frames;
+            size_t row;                     // its flush_timeline row
         };
         void flush();
         void warm_up();
@@ -210,6 +221,11 @@ class __attribute__((visibility("default"))) durable_log
         // half a segment), both segments together; bounded like the arenas
         std::atomic<uint64_t> m_ext_bytes;
         std::atomic<uint64_t> m_ext_peak;
+        // flush_timeline: rows of 7 (under m_mtx), times from m_t_open
+        std::vector<double> m_timeline;
+        std::chrono::steady_clock::time_point m_t_open;
+        double since_open() const;
+        void mark(size_t row, int col, double v);
 
     private:
         durable_log(const durable_log&);

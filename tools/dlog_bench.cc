@@ -279,6 +279,10 @@ int main(int argc, char** argv)
             },
             nullptr);
     log.set_fsync_delay_for_testing(fsync_delay);
+    // DLOG_PINNED=0/1: ordinary or pinned staging arenas whatever the engine
+    // (an injected engine defaults to ordinary memory, the GPU batch to pinned)
+    if (const char* e = getenv("DLOG_PINNED")) log.set_pinned_arenas_for_testing(atoi(e) != 0);
+    const double t_open = now();
     if (!log.open(dir))
     {
         fprintf(stderr, "open(%s) failed: %s\n", dir.c_str(), strerror(log.error()));
@@ -373,6 +377,23 @@ int main(int argc, char** argv)
     double fs[6], fm[6];
     log.flush_seconds(fs);
     log.flush_max_seconds(fm);
+    // DLOG_TIMELINE=path: the per-flush timeline (durable_log::flush_timeline)
+    // as text, after a header line with the run's own marks, all in seconds
+    // since open(): appends started, appends returned, everything durable
+    if (const char* tp = getenv("DLOG_TIMELINE"))
+        if (FILE* f = fopen(tp, "w"))
+        {
+            std::vector<double> rows(size_t(1 << 14) * 7);
+            const size_t nr = log.flush_timeline(rows.data(), size_t(1) << 14);
+            fprintf(f, "# start %.6f appended %.6f durable %.6f\n", t0 - t_open, t_appended - t_open,
+                    t_durable - t_open);
+            fprintf(f, "# sealed checksummed queued write_start write_end synced bytes\n");
+            for (size_t i = 0; i < nr; ++i)
+                fprintf(f, "%.6f %.6f %.6f %.6f %.6f %.6f %.0f\n", rows[i * 7], rows[i * 7 + 1],
+                        rows[i * 7 + 2], rows[i * 7 + 3], rows[i * 7 + 4], rows[i * 7 + 5],
+                        rows[i * 7 + 6]);
+            fclose(f);
+        }
 
     // the replay: every record back, in order, byte-exact
     Replay rp{&rec_len, &rec_at, pool.data()};

@@ -57,6 +57,14 @@ while [ $# -gt 0 ]; do
              timeout -k 10 120 python3 tools/mid_probe.py --lib tools/ab/libconsus_crc32c_$v.so --path window --mib ${WIN_MIB:-1,4,16} --reps 300 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }; grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd /"
            done; done | tee "$OUT/wskip.out" ;;
     errtests) run pytest_err 600 python -u -m pytest tests/test_gpu_errors.py tests/test_gpu_window.py -x -q --timeout 300 --timeout-method thread ;;
+    wghw) run wg_hw 300 python3 tools/wg_hw_probe.py tools/ab/libconsus_crc32c_stamp.so "$OUT/wg_hw.npz" --launches ${WGHW_LAUNCHES:-12} ;;
+    dlogtl) for rnd in 1 2 3; do for eng in ${DLOGTL_ENGINES:-gpu fake_pinned fake refscheme}; do
+              envs="DLOG_ENTRY=zipf DLOG_TIMELINE=$OUT/tl_${eng}_$rnd.txt"
+              case $eng in fake_pinned) envs="$envs FAKE_CRC=1 DLOG_PINNED=1";; fake) envs="$envs FAKE_CRC=1";;
+                refscheme) envs="$envs REF_CRC_SO=$ROOT/oracle/_ref/libref_crc32c.so REF_SCHEME=1";; gpu_unpinned) envs="$envs DLOG_PINNED=0";; esac
+              rm -rf /dev/shm/dltl; env $envs timeout -k 10 120 ./tools/dlog_bench /dev/shm/dltl 8 ${DLOGTL_PER:-25000} 0 0 > "$OUT/dl.out" 2> "$OUT/dl.err" || { cat "$OUT/dl.err"; rm -rf /dev/shm/dltl; exit 1; }
+              echo "round $rnd $eng $(cat "$OUT/dl.out")"
+            done; done > "$OUT/dlogtl.out"; rm -rf /dev/shm/dltl; cut -c1-200 "$OUT/dlogtl.out" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
     flush) run flush_probe 300 ./tools/flush_probe 1000 ;;
