@@ -1902,6 +1902,19 @@ constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a s
 constexpr uint32_t kSortFirst = 0x40000000u;  // ... its first piece (carries the init)
 constexpr uint32_t kSortRecMask = 0x3FFFFFFFu;
 constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
+// Entries (one 128-B line) between two workgroups' record-indexed regions
+// of the descriptor list: no line is shared by two regions (round 6, help).
+constexpr uint32_t kSortPad = 8;
+// A helper takes a range from another workgroup's list only while it has at
+// least this many groups left beyond the owner's grab count.
+constexpr uint32_t kHelpMin = 2;
+
+// A 16-B write-through (sc1) store: visible to other XCDs once the storing
+// wave's vmcnt has drained (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void store16_sc1(void* p, const uint4& v)
+{
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(make_u32x4(v)) : "memory");
+}
 
 uint32_t sorted_blocks(uint64_t count) { return uint32_t((count + kSortRecs - 1) / kSortRecs); }
 
@@ -2053,6 +2066,8 @@ struct SortShared
     uint32_t next_lane;        // lane items taken (64 per grab)
     uint32_t teams_done;       // waves whose team groups are done (finish overlap)
     uint32_t next_fin;         // finish-pass records taken
+    uint32_t n_multi;          // items of split records in this share (none: it may be helped)
+    uint32_t help[kBlock / 64][2];  // per wave, helping: the next and the end group of its range
     uint32_t lane_base;        // the first lane item's position among the last pieces
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
@@ -2489,7 +2504,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
-    uint32_t lrows, int fused, uint32_t bar_base)
+    uint32_t lrows, int fused, uint32_t bar_base, uint64_t* __restrict__ steal_ws, uint32_t epoch,
+    uint32_t help_delay)
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint64_t piece = uint64_t(1) << plog;
@@ -2501,6 +2517,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x == 0) S.next_lane = 0;
     if (threadIdx.x == 0) S.teams_done = 0;
     if (threadIdx.x == 0) S.next_fin = 0;
+    if (threadIdx.x == 0) S.n_multi = 0;
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
     // whole records finished in the loop (RB = 4, small batches) or by the
@@ -2611,15 +2628,28 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         return make_uint4(uint32_t(ps), uint32_t(ps >> 32), uint32_t(pe - ps),
                           uint32_t(r) | (f.s.n > 1 ? kSortMulti : 0u) | (head ? kSortFirst : 0u));
     };
-    uint4* const fullv = items + count;
-    uint4* const lastv = items + rlo;
+    // Workgroup b's record-indexed slots start 8 b entries (a 128-B line) past
+    // rlo, so no line of descriptors (or fold values) is shared by two
+    // workgroups' regions: a helping workgroup on another XCD reads a
+    // region's lines and must never hold a stale copy of one in its L2
+    // (round 6, helpers).  The full pieces' regions follow all of them.
+    const uint64_t pad = uint64_t(kSortPad) * blockIdx.x;
+    uint4* const fullv = items + count + uint64_t(kSortPad) * gridDim.x;
+    uint4* const lastv = items + rlo + pad;
     // absolute slots: full run at fpos, last piece at lpos
     // Descriptors go out with non-temporal stores: the ~2 MB of them per XCD
     // then do not sit dirty in the XCD's 4 MB L2 through the hash phase
     // (measured: prologue 8 us longer, step 8-10 us shorter).  The group loop
     // reads them two groups ahead (non-temporal loads there: neutral).
+    // A share that other workgroups may help with (round 6) writes its
+    // descriptors write-through (sc1; nt stores are not, MI355X_MICROARCH.md
+    // inter-workgroup visibility) for the helpers' sc1 loads.
+    bool helpable = false;
     auto put = [&](uint4* dst, const uint4& dv) {
-        __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
+        if (helpable)
+            store16_sc1(dst, dv);
+        else
+            __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
     };
     // Up to kLdsBytes / 16 items, the descriptors go to LDS at their list
     // position (the table image's space: the tables are staged after), and
@@ -2663,6 +2693,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                 const RecInfo f = info(r, av[u], Lv[u]);
                 uint32_t rf, rl;
                 take(f, rf, rl);
+                if (!second && f.s.n > 1 && (f.nf || f.last)) S.n_multi = 1u;  // a split record's items
                 if (second)
                     place(r, av[u], Lv[u], f, rf, rl);  // the bins hold cursors now
                 else if (held)
@@ -2699,7 +2730,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             const uint32_t fb = uint32_t(blockIdx.x * fpw);
             S.n_full = nf;
             S.n_items = nf + uint32_t(total);
-            if (nf > fpw || count + uint64_t(gridDim.x) * fpw > item_cap)
+            if (nf > fpw || count + uint64_t(gridDim.x) * (fpw + kSortPad) > item_cap)
             {
                 ctrl[1] = 1;  // workspace too small (understated total_bytes): out[] left alone
                 ctrl[2] = 1;  // sticky: an asynchronous batch's is reported at the next stream sync
@@ -2716,6 +2747,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     __syncthreads();
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     staged = n_items <= kLdsBytes / 16;
+    helpable = epoch != 0 && S.n_multi == 0;
     stage_nf = n_full;
     if (n_items)
     {
@@ -2749,13 +2781,36 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
         __syncthreads();
     }
-    stage_tables(tables);  // ends with a barrier
+    stage_tables(tables);  // ends with a barrier; every thread's descriptor stores are done
     SORT_STAMP(4);
     // team items first, lane items (positions n_long ..) after them
     const uint32_t n_long = n_full + S.lane_base;
 
     // (4) Groups of 8 team items, largest first, one LDS grab per group.
     const uint32_t n_groups = (n_long + 7) / 8;
+    // Help (round 6): a workgroup whose team groups are done takes groups
+    // from the END of another's list.  Every write of a helped group is
+    // idempotent -- a whole record's CRC, finished in the loop -- so a group
+    // done by both the owner and a helper is only wasted work, never wrong;
+    // a share with split records (whose pieces XOR into out[]) is never
+    // helped.  Per workgroup, in steal_ws (agent-scope words, this launch's
+    // epoch in the high half): [0] tail -- groups at or past it belong to
+    // helpers, lowered by their CAS; [1] the owner's grab count; [2] rlo and
+    // n_long of its list.  The owner's waves read the tail at each grab (the
+    // load issued one grab ahead) and stop at it; its finish pass covers the
+    // groups below the tail it reads after its team groups.
+#define SW_OWN (steal_ws + 4 * blockIdx.x)
+#define SW_EP (uint64_t(epoch) << 32)
+    if (epoch && threadIdx.x == 0)
+    {
+        uint64_t* const sw_own = SW_OWN;
+        const uint64_t ep = SW_EP;
+        __hip_atomic_store(sw_own + 2, (uint64_t(rlo) + pad) | (uint64_t(n_long) << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(sw_own, ep | (helpable ? n_groups : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t tw = lane / kTeam;
     const uint32_t li = lane_info();
@@ -2788,56 +2843,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
-    auto grab = [&]() {
-        uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(&S.next_group, 1u);
-        return uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
-    };
-    const uint4* const listF = items + count + S.full_base;  // full pieces first
-    const uint4* const listL = items + rlo - n_full;          // then the rest
-    auto load_desc = [&](uint32_t g) {
-        const uint32_t i = g * 8 + tw;
-        const uint4* p = (g < n_groups && i < n_long) ? (i < n_full ? listF : listL) + i
-                                                       : reinterpret_cast<const uint4*>(zero16);
-        return *p;
-    };
-    // Uniform shape of a group: n rows (its largest item, padded to an even
-    // count with a leading zero row), the first row of that item, the last
-    // row in which some team's item starts (or its init word spills into),
-    // and the first row from which every lane reads item bytes (n: never, in
-    // a group with teams but no item).  The list is descending except where
-    // the 512-row full pieces meet the 513-row whole records (the full
-    // pieces are listed first), so the largest and smallest item are taken
-    // over the group's teams, not from its first and last.
-    struct Shape
-    {
-        int32_t n, fmin, fedge, fast;
-    };
-    auto shape_of = [&](const uint4& d, uint32_t g) {
-        Shape s{0, 0, 0, 0};
-        if (g >= n_groups) return s;
-        const uint32_t tlast = min(7u, n_long - 1 - g * 8);
-        const int rv = int(sort_rows(d));
-        int32_t rmax = 0, rmin = int32_t(kSortRows);
-#pragma unroll
-        for (uint32_t t = 0; t < 8; ++t)
-        {
-            const int32_t x = __builtin_amdgcn_readlane(rv, int(t * kTeam));
-            rmax = t <= tlast ? max(rmax, x) : rmax;
-            rmin = t <= tlast ? min(rmin, x) : rmin;
-        }
-        s.n = (rmax + RB - 1) & ~(RB - 1);
-        s.fmin = s.n - rmax;
-        s.fedge = s.n - rmin + 1;
-        s.fast = tlast == 7 ? s.fedge + 1 : s.n;
-        return s;
-    };
-    auto row_ptr = [&](const SortView& v, int32_t r, bool fast) {
-        const uint8_t* p = reinterpret_cast<const uint8_t*>(v.p0 + uint64_t(uint32_t(r)) * kRowBytes);
-        if (!fast) p = (r >= v.lo && r <= v.hi) ? p : zero16;
-        return p;
-    };
-
+    const uint4* const listF = fullv + S.full_base;  // full pieces first
+    // The list the group loop runs (wave-uniform): this workgroup's own (full
+    // pieces at listF, the rest from srcL), then, helping, ranges of other
+    // workgroups' lists (no full pieces).  One set of registers for both:
+    // the own list's values are restored for the lane items and the finish.
+    // Only a workgroup without split records helps (its n_full is 0, so a
+    // helped list, which has no full pieces either, needs no other base).
+    const uint4* srcL = lastv - n_full;
+    uint32_t src_long = n_long, src_groups = n_groups;
+    uint32_t lim = n_groups;         // own list: groups from the tail on are the helpers'
+    uint64_t tail_ahead = SW_EP | n_groups;  // lane 0: the tail word, loaded a grab ahead
     // (5) Lane items, 64 per grab, one per lane (lane
     // items).  A lane hashes the 16-B aligned blocks its item touches with
     // the slice-by-16 tables: bytes before the item are zeroed (leading zeros
@@ -2851,8 +2867,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // longer item takes another round)
     constexpr int32_t kLaneBlocks = MI_SORT_LANE_BLOCKS;
     auto lane_items = [&]() {
-        const uint32_t n_lane = n_items - n_long;
-        const uint4* const listLane = listL + n_long;
+        // the own list's lane items (re-read: the group loop's registers held
+        // helped lists meanwhile)
+        const uint32_t n_lane = S.n_items - (S.n_full + S.lane_base);
+        const uint4* const listLane = lastv + S.lane_base;
         auto grab64 = [&]() {
             uint32_t c = 0;
             if (lane == 0) c = atomicAdd(&S.next_lane, 64u);
@@ -2955,179 +2973,362 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             d = d1;
         }
     };
-    uint32_t g_cur = grab();
-    uint4 d_cur = load_desc(g_cur);
-    uint32_t g_nxt = grab();
-    uint4 d_nxt = load_desc(g_nxt);
-    Shape shA = shape_of(d_cur, g_cur);
-    SortView vA = sort_view(d_cur, shA.n, tl, inits, ones_word);
-    const uint32_t slot0 = rlo - n_full + tw;  // slot of list position i: slot0 + 8 g (whole records)
-    vA.slot = slot0 + g_cur * 8;
-    Shape shB{0, 0, 0, 0};
-    SortView vB = vA;
-    const SortView& cur0 = vA;
-    // Row ring of RB buffers: row r of a group sits in b[r % RB]; each row
-    // step issues row r + RB - 1 (this group's, or one of the next group's
-    // first rows) before folding row r.  Groups are padded to a multiple of
-    // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
-    // flight per wave while another folds (measured on the headline batch:
-    // one row ahead costs < 1 % against three; here it keeps the padding to
-    // half a row per group).  RB = 4 serves small batches (pieces below
-    // 64 KiB), where a wave has only a group or two of up to 33 rows, so the
-    // rows in flight per wave, not the HBM, bound it; it finishes whole
-    // records in the loop (no finish pass).  RB = 8 (128 VGPRs once the
-    // finish pass is gone) measured no faster than 4 at 1 MiB - 2 GiB
-    // (round 4, profiles/r04_sorted_ring_sweep.txt).
-    uint4 b[RB];
-#pragma unroll
-    for (int j = 0; j < RB - 1; ++j) b[j] = load16_edge(row_ptr(cur0, j, false));
-    if (RB == 2 && shA.n == 2) b[1] = load16_edge(row_ptr(cur0, 1, false));
-    __builtin_amdgcn_sched_barrier(0);
-    // One group: hash `cur` (shape sh) while the next group's view is built
-    // into `nxt`.  The loop runs it twice per iteration with the two views
-    // swapped (round 2 A/B: profiles/r02_sorted_view32_pingpong_ab.txt), so the ~20 registers of a view are never
-    // copied at the back edge.
-    auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
-        // A 2-row group runs no body loop: its row 1 was issued at the end of
-        // the previous step, into b[1] once that step's last row was folded
-        // (see below), a whole fold, finish and group header ahead.
-        const bool pre = RB == 2 && sh.n == 2;
-        const uint32_t g_nn = grab();
-        const uint4 d_nn = load_desc(g_nn);
-        shn = shape_of(d_nxt, g_nxt);
-        nxt = sort_view(d_nxt, shn.n, tl, inits, ones_word);
-        nxt.slot = slot0 + g_nxt * 8;
-        uint32_t V[4] = {0, 0, 0, 0};
-        const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
-        // General row: padding skip, start mask and init word (rows up to
-        // fedge), end mask (row n - 1), zero-block reads.  Used for the first
-        // rows and the last RB of a group; the rows between take the body
-        // loop below: all lanes read item bytes, nothing to mask.
-        auto gen_row = [&](uint4 d, int32_t r) {
-            if (r < fmin) return;  // the padding row: V stays 0
-            if (r <= fedge)
-            {
-                // row f: (d & keep) ^ ~init in one v_bitop3 per dword (truth
-                // table index S0 S1 S2 = d keep x, MSB first: 0x6A)
-                const bool at_f = r == cur.f;
-                d.x = at_f ? __builtin_amdgcn_bitop3_b32(d.x, cur.kf.x, cur.xf.x, 0x6A) : d.x;
-                d.y = at_f ? __builtin_amdgcn_bitop3_b32(d.y, cur.kf.y, cur.xf.y, 0x6A) : d.y;
-                d.z = at_f ? __builtin_amdgcn_bitop3_b32(d.z, cur.kf.z, cur.xf.z, 0x6A) : d.z;
-                d.w = at_f ? __builtin_amdgcn_bitop3_b32(d.w, cur.kf.w, cur.xf.w, 0x6A) : d.w;
-                d.x ^= r == cur.f + 1 ? cur.xs : 0u;
-            }
-            if (r == n - 1)
-            {
-                d.x &= cur.ke.x;
-                d.y &= cur.ke.y;
-                d.z &= cur.ke.z;
-                d.w &= cur.ke.w;
-            }
-            if (r == fmin)
-                row_first(V, d);  // the largest item starts here; every other team's row is zero
-            else
-                row_update(V, d, li);
-        };
-        // body rows [hend, n - RB): after every team's first row and init
-        // word (full groups only: a partial group has teams without items)
-        const int32_t hend = fast < n ? min(n - RB, (fedge + RB) & ~(RB - 1)) : n - RB;
-        int32_t r = 0;
-        for (; r < hend; r += RB)
+    // Help (round 6): the widest remaining range of another workgroup's list
+    // (tail - grab count), a quarter of it taken from its end by one CAS on
+    // its tail word; false when none has kHelpMin groups left.
+    auto claim = [&]() -> bool {
+        for (int tries = 0; tries < 16; ++tries)
         {
-#pragma unroll
-            for (int j = 0; j < RB; ++j)
+            uint32_t best = 0, bv = 0, bprog = 0;
+            for (uint32_t v0 = 0; v0 < gridDim.x; v0 += 64)
             {
+                const uint32_t v = v0 + lane;
+                if (v < gridDim.x && v != blockIdx.x)
                 {
-                    const int32_t rr = r + j + RB - 1;
-                    const uint8_t* pp = row_ptr(cur, rr, false);
-                    b[(j + RB - 1) % RB] = rr <= fedge ? load16_edge(pp) : load16(pp);
+                    const uint64_t t = __hip_atomic_load(steal_ws + 4 * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t pr = __hip_atomic_load(steal_ws + 4 * v + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t rem = (t >> 32) == epoch && (pr >> 32) == epoch && uint32_t(t) > uint32_t(pr)
+                                             ? uint32_t(t) - uint32_t(pr) : 0u;
+                    if (rem > best)
+                    {
+                        best = rem;
+                        bv = v;
+                        bprog = uint32_t(pr);
+                    }
                 }
-                __builtin_amdgcn_sched_barrier(0);
-                gen_row(b[j], r + j);
+            }
+#pragma unroll
+            for (int dd = 32; dd >= 1; dd >>= 1)
+            {
+                const uint32_t ob = uint32_t(__shfl_xor(int(best), dd));
+                const uint32_t ov = uint32_t(__shfl_xor(int(bv), dd));
+                const uint32_t op = uint32_t(__shfl_xor(int(bprog), dd));
+                if (ob > best || (ob == best && ov < bv))
+                {
+                    best = ob;
+                    bv = ov;
+                    bprog = op;
+                }
+            }
+            if (best < kHelpMin) return false;
+            uint32_t lo = 0, hi = 0;
+            if (lane == 0)
+            {
+                uint64_t* const w = steal_ws + 4 * bv;
+                uint64_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                while ((old >> 32) == epoch && uint32_t(old) > bprog + 1)
+                {
+                    const uint32_t t = uint32_t(old);
+                    const uint32_t k = max(1u, (t - bprog) / 4);
+                    if (__hip_atomic_compare_exchange_strong(w, &old, old - k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT))
+                    {
+                        lo = t - k;
+                        hi = t;
+                        break;
+                    }
+                }
+            }
+            lo = uint32_t(__builtin_amdgcn_readfirstlane(int(lo)));
+            hi = uint32_t(__builtin_amdgcn_readfirstlane(int(hi)));
+            if (hi > lo)
+            {
+                // groups helped, all launches (mi_debug_sort_helped; tests)
+                if (lane == 0) __hip_atomic_fetch_add(ctrl + 6, hi - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t m = __hip_atomic_load(steal_ws + 4 * bv + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t m_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(m))));
+                src_long = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(m >> 32))));
+                srcL = items + m_lo;
+                src_groups = (src_long + 7) / 8;
+                if (lane == 0)
+                {
+                    S.help[threadIdx.x >> 6][0] = lo;
+                    S.help[threadIdx.x >> 6][1] = hi;
+                }
+                return true;
             }
         }
-        {
-            const uint8_t* pr = reinterpret_cast<const uint8_t*>(cur.p0);
-            for (; r < n - RB; r += RB)
+        return false;
+    };
+    // The group loop, instantiated twice: the own list (HELP false), and a
+    // range of another workgroup's list (HELP true: sc0 sc1 descriptor loads,
+    // every record finished in the loop, the range from LDS).  Two copies of
+    // the code, but neither carries the other's state in its registers.
+    auto groups = [&](auto help_tag) {
+        constexpr bool helping = decltype(help_tag)::value;
+        auto grab = [&]() {
+            if (helping)
             {
-#pragma unroll
+                // this wave's helped range, kept in LDS (no registers across the loop)
+                const uint32_t hn = S.help[threadIdx.x >> 6][0], he = S.help[threadIdx.x >> 6][1];
+                if (hn >= he) return src_groups;
+                if (lane == 0) S.help[threadIdx.x >> 6][0] = hn + 1;
+                return uint32_t(__builtin_amdgcn_readfirstlane(int(hn)));
+            }
+            uint32_t g = 0;
+            if (lane == 0) g = atomicAdd(&S.next_group, 1u);
+            g = uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
+            if (helpable)
+            {
+                // a word of an earlier launch (this launch's not yet stored) is ignored
+                const uint32_t t_ep = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(tail_ahead >> 32))));
+                const uint32_t t_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(tail_ahead))));
+                if (t_ep == epoch) lim = min(lim, t_lo);
+                if (lane == 0)
+                {
+                    tail_ahead = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(SW_OWN + 1, SW_EP | (g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (g >= lim) g = n_groups;  // a helper's
+            }
+            return g;
+        };
+        auto load_desc = [&](uint32_t g) {
+            const uint32_t i = g * 8 + tw;
+            const bool in = g < src_groups && i < src_long;
+            const uint4* p = in ? (i < n_full ? listF : srcL) + i : reinterpret_cast<const uint4*>(zero16);
+            if (helping)
+            {
+                // another workgroup's list, stored sc1 this launch: a volatile
+                // (sc0 sc1) load, never served from a stale line of this L1/L2
+                typedef const volatile __attribute__((address_space(1))) u32x4_t* vgptr;
+                const u32x4_t v = *(vgptr)(uintptr_t)p;
+                return make_uint4(v.x, v.y, v.z, v.w);
+            }
+            return *p;
+        };
+        // Uniform shape of a group: n rows (its largest item, padded to an even
+        // count with a leading zero row), the first row of that item, the last
+        // row in which some team's item starts (or its init word spills into),
+        // and the first row from which every lane reads item bytes (n: never, in
+        // a group with teams but no item).  The list is descending except where
+        // the 512-row full pieces meet the 513-row whole records (the full
+        // pieces are listed first), so the largest and smallest item are taken
+        // over the group's teams, not from its first and last.
+        struct Shape
+        {
+            int32_t n, fmin, fedge, fast;
+        };
+        auto shape_of = [&](const uint4& d, uint32_t g) {
+            Shape s{0, 0, 0, 0};
+            if (g >= src_groups) return s;
+            const uint32_t tlast = min(7u, src_long - 1 - g * 8);
+            const int rv = int(sort_rows(d));
+            int32_t rmax = 0, rmin = int32_t(kSortRows);
+    #pragma unroll
+            for (uint32_t t = 0; t < 8; ++t)
+            {
+                const int32_t x = __builtin_amdgcn_readlane(rv, int(t * kTeam));
+                rmax = t <= tlast ? max(rmax, x) : rmax;
+                rmin = t <= tlast ? min(rmin, x) : rmin;
+            }
+            s.n = (rmax + RB - 1) & ~(RB - 1);
+            s.fmin = s.n - rmax;
+            s.fedge = s.n - rmin + 1;
+            s.fast = tlast == 7 ? s.fedge + 1 : s.n;
+            return s;
+        };
+        auto row_ptr = [&](const SortView& v, int32_t r, bool fast) {
+            const uint8_t* p = reinterpret_cast<const uint8_t*>(v.p0 + uint64_t(uint32_t(r)) * kRowBytes);
+            if (!fast) p = (r >= v.lo && r <= v.hi) ? p : zero16;
+            return p;
+        };
+
+        const uint32_t slot0 = uint32_t(rlo + pad) - n_full + tw;  // slot of list position i: slot0 + 8 g (whole records)
+        uint32_t g_nxt;
+        uint4 d_nxt;
+        Shape shA, shB;
+        SortView vA, vB;
+        // Row ring of RB buffers: row r of a group sits in b[r % RB]; each row
+        // step issues row r + RB - 1 (this group's, or one of the next group's
+        // first rows) before folding row r.  Groups are padded to a multiple of
+        // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
+        // flight per wave while another folds (measured on the headline batch:
+        // one row ahead costs < 1 % against three; here it keeps the padding to
+        // half a row per group).  RB = 4 serves small batches (pieces below
+        // 64 KiB), where a wave has only a group or two of up to 33 rows, so the
+        // rows in flight per wave, not the HBM, bound it; it finishes whole
+        // records in the loop (no finish pass).  RB = 8 (128 VGPRs once the
+        // finish pass is gone) measured no faster than 4 at 1 MiB - 2 GiB
+        // (round 4, profiles/r04_sorted_ring_sweep.txt).
+        uint4 b[RB];
+        // the first two groups of a list, the ring's first rows
+        auto prime = [&]() {
+            const uint32_t g_cur = grab();
+            const uint4 d_cur = load_desc(g_cur);
+            g_nxt = grab();
+            d_nxt = load_desc(g_nxt);
+            shA = shape_of(d_cur, g_cur);
+            vA = sort_view(d_cur, shA.n, tl, inits, ones_word);
+            vA.slot = slot0 + g_cur * 8;
+            shB = Shape{0, 0, 0, 0};
+            vB = vA;
+    #pragma unroll
+            for (int j = 0; j < RB - 1; ++j) b[j] = load16_edge(row_ptr(vA, j, false));
+            if (RB == 2 && shA.n == 2) b[1] = load16_edge(row_ptr(vA, 1, false));
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // One group: hash `cur` (shape sh) while the next group's view is built
+        // into `nxt`.  The loop runs it twice per iteration with the two views
+        // swapped (round 2 A/B: profiles/r02_sorted_view32_pingpong_ab.txt), so the ~20 registers of a view are never
+        // copied at the back edge.
+        auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
+            // A 2-row group runs no body loop: its row 1 was issued at the end of
+            // the previous step, into b[1] once that step's last row was folded
+            // (see below), a whole fold, finish and group header ahead.
+            const bool pre = RB == 2 && sh.n == 2;
+            const uint32_t g_nn = grab();
+            const uint4 d_nn = load_desc(g_nn);
+            shn = shape_of(d_nxt, g_nxt);
+            nxt = sort_view(d_nxt, shn.n, tl, inits, ones_word);
+            nxt.slot = slot0 + g_nxt * 8;
+            uint32_t V[4] = {0, 0, 0, 0};
+            const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
+            // General row: padding skip, start mask and init word (rows up to
+            // fedge), end mask (row n - 1), zero-block reads.  Used for the first
+            // rows and the last RB of a group; the rows between take the body
+            // loop below: all lanes read item bytes, nothing to mask.
+            auto gen_row = [&](uint4 d, int32_t r) {
+                if (r < fmin) return;  // the padding row: V stays 0
+                if (r <= fedge)
+                {
+                    // row f: (d & keep) ^ ~init in one v_bitop3 per dword (truth
+                    // table index S0 S1 S2 = d keep x, MSB first: 0x6A)
+                    const bool at_f = r == cur.f;
+                    d.x = at_f ? __builtin_amdgcn_bitop3_b32(d.x, cur.kf.x, cur.xf.x, 0x6A) : d.x;
+                    d.y = at_f ? __builtin_amdgcn_bitop3_b32(d.y, cur.kf.y, cur.xf.y, 0x6A) : d.y;
+                    d.z = at_f ? __builtin_amdgcn_bitop3_b32(d.z, cur.kf.z, cur.xf.z, 0x6A) : d.z;
+                    d.w = at_f ? __builtin_amdgcn_bitop3_b32(d.w, cur.kf.w, cur.xf.w, 0x6A) : d.w;
+                    d.x ^= r == cur.f + 1 ? cur.xs : 0u;
+                }
+                if (r == n - 1)
+                {
+                    d.x &= cur.ke.x;
+                    d.y &= cur.ke.y;
+                    d.z &= cur.ke.z;
+                    d.w &= cur.ke.w;
+                }
+                if (r == fmin)
+                    row_first(V, d);  // the largest item starts here; every other team's row is zero
+                else
+                    row_update(V, d, li);
+            };
+            // body rows [hend, n - RB): after every team's first row and init
+            // word (full groups only: a partial group has teams without items)
+            const int32_t hend = fast < n ? min(n - RB, (fedge + RB) & ~(RB - 1)) : n - RB;
+            int32_t r = 0;
+            for (; r < hend; r += RB)
+            {
+    #pragma unroll
                 for (int j = 0; j < RB; ++j)
                 {
-                    b[(j + RB - 1) % RB] = load16(pr + uint32_t(r + j + RB - 1) * uint32_t(kRowBytes));
+                    {
+                        const int32_t rr = r + j + RB - 1;
+                        const uint8_t* pp = row_ptr(cur, rr, false);
+                        b[(j + RB - 1) % RB] = rr <= fedge ? load16_edge(pp) : load16(pp);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
-                    row_update(V, b[j], li);
+                    gen_row(b[j], r + j);
                 }
             }
-        }
-        // the last RB rows: row n - 1, then the next group's first rows
-#pragma unroll
-        for (int j = 0; j < RB; ++j)
+            {
+                const uint8_t* pr = reinterpret_cast<const uint8_t*>(cur.p0);
+                for (; r < n - RB; r += RB)
+                {
+    #pragma unroll
+                    for (int j = 0; j < RB; ++j)
+                    {
+                        b[(j + RB - 1) % RB] = load16(pr + uint32_t(r + j + RB - 1) * uint32_t(kRowBytes));
+                        __builtin_amdgcn_sched_barrier(0);
+                        row_update(V, b[j], li);
+                    }
+                }
+            }
+            // the last RB rows: row n - 1, then the next group's first rows
+    #pragma unroll
+            for (int j = 0; j < RB; ++j)
+            {
+                if (!(j == 0 && pre))
+                    b[(j + RB - 1) % RB] = load16_edge(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
+                __builtin_amdgcn_sched_barrier(0);
+                gen_row(b[j], n - RB + j);
+            }
+            // the next group's row 1 if it has two rows (b[1] is free now)
+            if (RB == 2 && shn.n == 2) b[1] = load16_edge(row_ptr(nxt, 1, false));
+            const uint32_t W = team_fold(V);
+            flush();  // the previous group's split-record pieces
+            {
+                const bool multi = cur.recf != kSortNone && (cur.recf & kSortMulti);
+                // whole records: the fold value by slot, eight consecutive words per
+                // group (stores to out[rec] here hit a line per record, scattered:
+                // 8-11 us of the configs[2] step, profiles/r03_sorted_late_finish_ab.txt)
+                if (!INLOOP && !helping)
+                {
+                    if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
+                }
+                else if (cur.recf != kSortNone && !multi)
+                {
+                    // small batches (RB >= 4): a wave has a group or two, so the
+                    // finish pass's two dependent global reads per record cost
+                    // more than finishing here: crc = ~Z_{-m}(W) from LDS tables.
+                    // A helped group (another workgroup's) is finished here too.
+                    const uint32_t m = cur.m & 127u, nn = 128u - m;
+                    uint32_t t = zT_n(W, nn & 15u);
+                    t = (nn & 16u) ? zT<4>(t) : t;
+                    t = (nn & 32u) ? zG(kLdsZ32, t) : t;
+                    t = (nn & 64u) ? zG(kLdsZ64, t) : t;
+                    t = zG(kLdsZInv, t);
+                    if (tl == 0) out[cur.recf & kSortRecMask] = ~(m ? t : W);
+                }
+                p_multi = __builtin_amdgcn_ballot_w64(multi) != 0;
+                if (p_multi)
+                {
+                    // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
+                    const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
+                    const uint32_t q = tl & 3u;
+                    uint32_t pz_new = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
+                    // an opaque definition: without it the loop-carried copy of pz at
+                    // the loop header waited for this load every group
+                    asm volatile("" : "+v"(pz_new));
+                    pz = pz_new;
+                }
+                p_recf = multi ? cur.recf : kSortNone;
+                p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;
+            }
+            g_nxt = g_nn;
+            d_nxt = d_nn;
+        };
+        // twice per iteration with the two views swapped: the ~20 registers of a
+        // view are never copied at the back edge (~60 v_mov per group before)
+        prime();
+        while (shA.n > 0)
         {
-            if (!(j == 0 && pre))
-                b[(j + RB - 1) % RB] = load16_edge(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
-            __builtin_amdgcn_sched_barrier(0);
-            gen_row(b[j], n - RB + j);
+            step(vA, shA, vB, shB);
+            if (shB.n <= 0) break;
+            step(vB, shB, vA, shA);
         }
-        // the next group's row 1 if it has two rows (b[1] is free now)
-        if (RB == 2 && shn.n == 2) b[1] = load16_edge(row_ptr(nxt, 1, false));
-        const uint32_t W = team_fold(V);
-        flush();  // the previous group's split-record pieces
-        {
-            const bool multi = cur.recf != kSortNone && (cur.recf & kSortMulti);
-            // whole records: the fold value by slot, eight consecutive words per
-            // group (stores to out[rec] here hit a line per record, scattered:
-            // 8-11 us of the configs[2] step, profiles/r03_sorted_late_finish_ab.txt)
-            if (!INLOOP)
-            {
-                if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
-            }
-            else if (cur.recf != kSortNone && !multi)
-            {
-                // small batches (RB >= 4): a wave has a group or two, so the
-                // finish pass's two dependent global reads per record cost
-                // more than finishing here: crc = ~Z_{-m}(W) from LDS tables
-                const uint32_t m = cur.m & 127u, nn = 128u - m;
-                uint32_t t = zT_n(W, nn & 15u);
-                t = (nn & 16u) ? zT<4>(t) : t;
-                t = (nn & 32u) ? zG(kLdsZ32, t) : t;
-                t = (nn & 64u) ? zG(kLdsZ64, t) : t;
-                t = zG(kLdsZInv, t);
-                if (tl == 0) out[cur.recf & kSortRecMask] = ~(m ? t : W);
-            }
-            p_multi = __builtin_amdgcn_ballot_w64(multi) != 0;
-            if (p_multi)
-            {
-                // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
-                const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
-                const uint32_t q = tl & 3u;
-                uint32_t pz_new = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
-                // an opaque definition: without it the loop-carried copy of pz at
-                // the loop header waited for this load every group
-                asm volatile("" : "+v"(pz_new));
-                pz = pz_new;
-            }
-            p_recf = multi ? cur.recf : kSortNone;
-            p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;
-        }
-        g_nxt = g_nn;
-        d_nxt = d_nn;
-    };
-    // twice per iteration with the two views swapped: the ~20 registers of a
-    // view are never copied at the back edge (~60 v_mov per group before)
-    while (shA.n > 0)
-    {
-        step(vA, shA, vB, shB);
-        if (shB.n <= 0) break;
-        step(vB, shB, vA, shA);
-    }
-    flush();
+        flush();
 #if MI_SORT_FIN_OVERLAP
-    // this wave's fold values (wr) are stored: count it done for the finish
-    // pass, which starts when every wave's team groups are, beside the other
-    // waves' lane items
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) atomicAdd(&S.teams_done, 1u);
+        // this wave's fold values (wr) are stored: count it done for the
+        // finish pass, which starts when every wave's team groups are, beside
+        // the other waves' lane items (and help)
+        if (!helping)
+        {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) atomicAdd(&S.teams_done, 1u);
+        }
 #endif
+    };
+    // tests: workgroup 0 starts its list help_delay us late, so that the
+    // others run out first and help it (MI_CRC32C_SORT_HELP_DELAY_US)
+    if (help_delay && blockIdx.x == 0)
+    {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < uint64_t(help_delay) * 100u) __builtin_amdgcn_s_sleep(8);
+    }
+    groups(std::integral_constant<bool, false>{});
+    if (helpable)
+        while (claim()) groups(std::integral_constant<bool, true>{});
     SORT_STAMP(5);
     lane_items();
     SORT_STAMP(6);
@@ -3150,8 +3351,15 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         __builtin_amdgcn_s_sleep(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     constexpr uint32_t FU = 4;
-    const uint32_t n_whole = n_long - n_full;
-    const uint4* const dl = items + rlo;
+    // whole records in groups at or past the tail were helped (finished by
+    // their helpers); every group below it was done here (round 6)
+    uint32_t n_whole = S.lane_base;  // n_long - n_full
+    if (helpable)
+    {
+        const uint64_t t = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((t >> 32) == epoch) n_whole = min(n_whole, 8u * uint32_t(t));
+    }
+    const uint4* const dl = lastv;
     for (;;)
     {
         uint32_t c0 = 0;
@@ -3165,7 +3373,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             const uint32_t k = c0 + u * 64 + lane;
             dv[u] = k < n_whole ? dl[k] : make_uint4(0, 0, 0, kSortMulti);
-            wv[u] = k < n_whole ? wr[uint64_t(rlo) + k] : 0u;
+            wv[u] = k < n_whole ? wr[uint64_t(rlo) + pad + k] : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
@@ -3187,8 +3395,15 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     __syncthreads();  // the workgroup's own stores are visible to it past the barrier
     constexpr uint32_t FU = 4;
-    const uint32_t n_whole = n_long - n_full;
-    const uint4* const dl = items + rlo;
+    // whole records in groups at or past the tail were helped (finished by
+    // their helpers); every group below it was done here (round 6)
+    uint32_t n_whole = S.lane_base;  // n_long - n_full
+    if (helpable)
+    {
+        const uint64_t t = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((t >> 32) == epoch) n_whole = min(n_whole, 8u * uint32_t(t));
+    }
+    const uint4* const dl = lastv;
     for (uint32_t k0 = threadIdx.x; k0 < n_whole; k0 += FU * kBlock)
     {
         uint4 dv[FU];
@@ -3198,7 +3413,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             const uint32_t k = k0 + u * kBlock;
             dv[u] = k < n_whole ? dl[k] : make_uint4(0, 0, 0, kSortMulti);
-            wv[u] = k < n_whole ? wr[uint64_t(rlo) + k] : 0u;
+            wv[u] = k < n_whole ? wr[uint64_t(rlo) + pad + k] : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
@@ -3262,13 +3477,14 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base);
+                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base, ws.steal, ws.steal_epoch,
+                       ws.help_delay);
     return hipGetLastError();
 }
 
 uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid)
 {
-    return count + uint64_t(grid) * sorted_full_per_wg(count, total_bytes, plog, grid);
+    return count + uint64_t(grid) * (sorted_full_per_wg(count, total_bytes, plog, grid) + kSortPad);
 }
 
 // ---------------------------------------------------------------------------
