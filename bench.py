@@ -435,14 +435,25 @@ def run_dlog(args, compact: bool = False) -> dict:
     threads = 8
     from oracle.oracle import REF_SO, reference_available
     workloads = [("uniform", {"per": 400_000, "lo": 42, "hi": 1024, "env": {},
-                              "what": "entry lengths uniform 42-1024 B"}),
+                              "what": "entry lengths uniform 42-1024 B; segment files on tmpfs"}),
                  ("zipf", {"per": 25_000, "lo": 0, "hi": 0, "env": {"DLOG_ENTRY": "zipf"},
-                           "what": "entry lengths of configs[2]: Zipf 64 B - 64 KiB"})]
+                           "what": "entry lengths of configs[2]: Zipf 64 B - 64 KiB; segment files "
+                                   "on tmpfs"}),
+                 # round 6: storage faster than the front-end (the writer's pwrite and
+                 # the fsync skipped): the log's rate is its appenders' and its
+                 # checksum's, which is where the checksum's placement shows
+                 ("zipf_sink", {"per": 25_000, "lo": 0, "hi": 0,
+                                "env": {"DLOG_ENTRY": "zipf", "DLOG_SINK": "1"},
+                                "what": "entry lengths of configs[2]; storage faster than the "
+                                        "front-end (pwrite and fsync skipped, no replay)"})]
+    # every engine stages frames in the same pinned arenas (round 6: with
+    # ordinary memory the CPU engines' appenders page-faulted their arenas and
+    # flushed smaller segments, a different log configuration)
     engines = [("gpu", {})]
     if reference_available() and not args.no_cpu:
-        engines.append(("reference-scheme", {"REF_CRC_SO": REF_SO, "REF_SCHEME": "1"}))
-        engines.append(("reference-cpu", {"REF_CRC_SO": REF_SO}))
-    engines.append(("no-checksum", {"FAKE_CRC": "1"}))
+        engines.append(("reference-scheme", {"REF_CRC_SO": REF_SO, "REF_SCHEME": "1", "DLOG_PINNED": "1"}))
+        engines.append(("reference-cpu", {"REF_CRC_SO": REF_SO, "DLOG_PINNED": "1"}))
+    engines.append(("no-checksum", {"FAKE_CRC": "1", "DLOG_PINNED": "1"}))
     nruns = max(7, args.steps // 4)
     # BENCH_DLOG_SCALE: fewer appends per run (CPU rehearsals of this leg only)
     scale = float(os.environ.get("BENCH_DLOG_SCALE", "1"))
@@ -458,6 +469,8 @@ def run_dlog(args, compact: bool = False) -> dict:
                     env = dict(os.environ)
                     env.update(w["env"])
                     env.update(extra)
+                    if runs[wname][name] or wname != workloads[0][0]:
+                        env["DLOG_NO_PROBES"] = "1"  # the GPU engine's one-off probes: first run only
                     r = subprocess.run([exe, os.path.join(d, "log"), str(threads), str(w["per"]),
                                         str(w["lo"]), str(w["hi"])],
                                        capture_output=True, text=True, timeout=300, env=env)
@@ -508,9 +521,12 @@ def run_dlog(args, compact: bool = False) -> dict:
     for wname, w in workloads:
         eng = {name: summary(runs[wname][name]) for name, _ in engines}
         res = {"workload": f"{threads} threads x {w['per']} appends, {w['what']}; then wait for "
-                           f"the watermark; segment files on tmpfs", "engines": eng}
+                           f"the watermark", "engines": eng}
         res["gpu_vs"] = {name: versus(eng["gpu"], eng[name]) for name, _ in engines if name != "gpu"}
-        best = median_run(runs[wname]["gpu"])
+        best = dict(median_run(runs[wname]["gpu"]))
+        first = runs[workloads[0][0]]["gpu"][0]  # the one run that took the engine's probes
+        for k in ("empty_batch_us", "cpu_batch_us", "link_us"):
+            best[k] = first.get(k, best.get(k))
         pf = per_flush(best)
         # The per-flush bound: the cheaper of the two routes the log chooses
         # between by size (durable_log.cc host_batch_max).  The GPU batch's:
@@ -560,12 +576,14 @@ def run_dlog(args, compact: bool = False) -> dict:
             "ms_per_step": round(median_run(runs["uniform"]["gpu"])["durable_s"] * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: splitmix64 entry bytes; uniform 42-1024 B and Zipf 64 B-64 KiB lengths",
-            "config": {"workload": "8 appending threads; two entry-length workloads; "
+            "config": {"workload": "8 appending threads; uniform and Zipf entries on tmpfs, Zipf "
+                                   "entries on a sink faster than the front-end; "
                                    f"{nruns} interleaved runs per engine and workload"},
             "workloads": out, "roofline": None, "cpu_baseline": cpu,
             "digest_verified": all(x["replayed"] == x["appends"] and x["replay_bad"] == 0
-                                   for w in runs.values() for name, rs in w.items()
-                                   if name != "no-checksum" for x in rs)}
+                                   for wn, w in runs.items() for name, rs in w.items()
+                                   if name != "no-checksum" and not wn.endswith("_sink")
+                                   for x in rs)}
 
 
 def run_secondary(args, E, traffic=(None, "skipped")) -> dict:
@@ -1038,7 +1056,7 @@ def _compact_cpu(c: dict | None, sample_chars: int = 120) -> dict | None:
     r = _pick(c, ("value", "unit", "cores", "kind", "single_thread_value", "matches_gpu", "error"))
     if "sample" in c:
         # the sample's first clause (what was hashed); the rest is in the detail file
-        s = c["sample"].split(", consus::crc32c")[0].split("; ")[0]
+        s = c["sample"].split(", consus::crc32c")[0].split("; ")[0].split(" (")[0]
         r["sample"] = s if len(s) <= sample_chars else s[:sample_chars - 3] + "..."
     return r
 
@@ -1063,7 +1081,7 @@ def _compact_secondary(r: dict) -> dict:
 def _compact_mid(r: dict) -> dict:
     if "batches" not in r:
         return r
-    return {"unit": r.get("unit"), "reps": r.get("reps"), "workload": r.get("workload"),
+    return {"reps": r.get("reps"), "workload": "configs[2] records cut to N MiB",
             "cols": ["mib", "us_per_batch", "gb_s", "path", "crc_ok"],
             "batches": [[b["mib"], b["us_per_batch"], b["gb_s"], b["path"], b["crc_ok"]]
                         for b in r["batches"]],
@@ -1078,9 +1096,9 @@ def _compact_dlog(r: dict) -> dict:
         return r
     out = _pick(r, ("value", "unit", "steps", "digest_verified"))
     out["metric"] = "durable-log appends/s, 8 appending threads"
-    out["cols"] = "appends/s median q1 q3, durable-latency us p50 p99"
+    out["cols"] = "appends/s median, durable-latency us p50 p99 (IQRs: detail file)"
     for wname, w in r["workloads"].items():
-        e = {name: [round(s["appends_per_s"][q]) for q in ("median", "q1", "q3")] +
+        e = {name: [round(s["appends_per_s"]["median"])] +
              [round(s["durable_latency_us"][q]) for q in ("p50_median", "p99_median")]
              for name, s in w["engines"].items()}
         f = w.get("flush", {})
@@ -1090,11 +1108,8 @@ def _compact_dlog(r: dict) -> dict:
                        for k, v in w.get("gpu_vs", {}).items()},
             "flush": dict(_pick(f, ("flushes", "host_flushes", "frame_bytes_per_flush",
                                     "batch_crc_vs_bound")),
-                          us_per_flush=_pick(f.get("us_per_flush", {}),
-                                             ("walk", "batch_crc", "patch", "pwrite")))}
-    out["cpu_baseline"] = _compact_cpu(r.get("cpu_baseline"), 100)
-    if out["cpu_baseline"]:
-        out["cpu_baseline"]["sample"] = "engine reference-scheme, uniform workload"
+                          us_per_flush=_pick(f.get("us_per_flush", {}), ("batch_crc", "pwrite")))}
+    out["cpu_baseline"] = "engines.reference-scheme (the detail file has it in full)"
     out["leg_wall_s"] = r.get("leg_wall_s")
     return out
 

@@ -107,6 +107,11 @@ class __attribute__((visibility("default"))) durable_log
         void flush_max_seconds(double out[6]) const;
         // Test hook: every fsync also sleeps this long (a slow disk on tmpfs).
         void set_fsync_delay_for_testing(uint32_t microseconds);
+        // Bench hook (call before open): the writer and the sync thread skip
+        // pwrite and fsync (storage faster than the appenders and the
+        // checksum), so the log's rate is its front-end's; the files stay
+        // empty (no replay).
+        void set_sink_for_testing(bool sink);
         // Most bytes of oversized frames (staged outside the arenas) held at
         // once: at most max(2 x segment capacity, 16 MiB, the largest such
         // frame).
@@ -217,6 +222,7 @@ class __attribute__((visibility("default"))) durable_log
         bool m_stop_writer;             // under m_mtx: the destructor ends the writer thread
         bool m_stop;                    // under m_mtx: the destructor ends the sync thread
         std::atomic<uint32_t> m_fsync_delay_us;
+        bool m_sink;                    // bench hook: no pwrite, no fsync
         // bytes of frames staged outside the arenas (entries of more than
         // half a segment), both segments together; bounded like the arenas
         std::atomic<uint64_t> m_ext_bytes;

@@ -22,6 +22,9 @@ bench = _bench_rank.bench
 with open(os.path.join(HERE, "..", "profiles", "r05_bench_default_session_r05bs.json")) as f:
     FULL = json.loads(f.read().strip().splitlines()[-1])
 LEG_OF = {"zipf": "config2_zipf", "stream": "config4_stream", "pcie4k": "config1_pcie_inclusive"}
+# round 6: the durable-log leg has a third workload (storage faster than the
+# front-end) of the same shape as the zipf one
+FULL["durable_log"]["workloads"]["zipf_sink"] = copy.deepcopy(FULL["durable_log"]["workloads"]["zipf"])
 
 
 def _leg(args, E, traffic=None):

@@ -149,7 +149,8 @@ int main(int argc, char** argv)
     // the floor of one flush's GPU batch: the round trip of a one-frame batch
     // from mapped pinned memory through the log's engine entry point
     double empty_us = 0;
-    if (!g_ref && !fake)
+    // DLOG_NO_PROBES=1: skip these one-off probes (repeated runs of a bench)
+    if (!g_ref && !fake && !(getenv("DLOG_NO_PROBES") && atoi(getenv("DLOG_NO_PROBES"))))
     {
         void* pin = nullptr;
         if (mi_host_malloc_pinned(&pin, 4096) == MI_CRC32C_OK)
@@ -282,6 +283,10 @@ int main(int argc, char** argv)
     // DLOG_PINNED=0/1: ordinary or pinned staging arenas whatever the engine
     // (an injected engine defaults to ordinary memory, the GPU batch to pinned)
     if (const char* e = getenv("DLOG_PINNED")) log.set_pinned_arenas_for_testing(atoi(e) != 0);
+    // DLOG_SINK=1: no pwrite, no fsync (storage faster than the front-end);
+    // nothing to replay then
+    const bool sink = getenv("DLOG_SINK") && atoi(getenv("DLOG_SINK"));
+    if (sink) log.set_sink_for_testing(true);
     const double t_open = now();
     if (!log.open(dir))
     {
@@ -397,7 +402,7 @@ int main(int argc, char** argv)
 
     // the replay: every record back, in order, byte-exact
     Replay rp{&rec_len, &rec_at, pool.data()};
-    const int64_t n = fake ? int64_t(total) : log.replay(
+    const int64_t n = fake || sink ? int64_t(total) : log.replay(
         [](void* p, const unsigned char* data, size_t len) {
             Replay* r = static_cast<Replay*>(p);
             const uint64_t i = r->next++;
@@ -428,7 +433,7 @@ int main(int argc, char** argv)
         cpu += b;
     }
     cpu += "}";
-    printf("{\"engine\": \"%s\", \"entries\": \"%s\", \"host_flushes\": %llu, \"cpu_batch_us\": %s, \"link_us\": %s, \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
+    printf("{\"sink\": %s, \"engine\": \"%s\", \"entries\": \"%s\", \"host_flushes\": %llu, \"cpu_batch_us\": %s, \"link_us\": %s, \"empty_batch_us\": %.2f, \"threads\": %d, \"appends\": %llu, \"entry_bytes\": %llu, \"frame_bytes\": %llu, "
            "\"append_s\": %.6f, \"durable_s\": %.6f, \"appends_per_s\": %.1f, "
            "\"frame_GiB_per_s\": %.4f, \"flushes\": %llu, \"frames_flushed\": %llu, "
            "\"failures\": %llu, \"error\": %d, \"replayed\": %lld, \"replay_bad\": %llu, "
@@ -438,7 +443,7 @@ int main(int argc, char** argv)
            "\"patch\": %.1f, \"pwrite\": %.1f, \"fsync\": %.1f}, "
            "\"durable_latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, "
            "\"max_at_s\": %.4f, \"samples\": %zu}}\n",
-           fake ? "none" : g_ref ? (ref_scheme ? "reference-scheme" : "reference-cpu") : "gpu",
+           sink ? "true" : "false", fake ? "none" : g_ref ? (ref_scheme ? "reference-scheme" : "reference-cpu") : "gpu",
            zipf ? "zipf 64 B - 64 KiB" : "uniform", (unsigned long long)host_flushes, cpu.c_str(), link.c_str(),
            empty_us, threads,
            (unsigned long long)total,
