@@ -2987,13 +2987,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                 {
                     const uint64_t t = __hip_atomic_load(steal_ws + 4 * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint64_t pr = __hip_atomic_load(steal_ws + 4 * v + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t rem = (t >> 32) == epoch && (pr >> 32) == epoch && uint32_t(t) > uint32_t(pr)
-                                             ? uint32_t(t) - uint32_t(pr) : 0u;
+                    // no grab of this launch yet: progress 0 (a late workgroup)
+                    const uint32_t pg = (pr >> 32) == epoch ? uint32_t(pr) : 0u;
+                    const uint32_t rem = (t >> 32) == epoch && uint32_t(t) > pg ? uint32_t(t) - pg : 0u;
                     if (rem > best)
                     {
                         best = rem;
                         bv = v;
-                        bprog = uint32_t(pr);
+                        bprog = pg;
                     }
                 }
             }
