@@ -2646,7 +2646,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // inter-workgroup visibility) for the helpers' sc1 loads.
     bool helpable = false;
     auto put = [&](uint4* dst, const uint4& dv) {
-        if (helpable)
+        if (helpable && !(help_delay & (8u << 16)))
             store16_sc1(dst, dv);
         else
             __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
@@ -3077,8 +3077,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                 if (t_ep == epoch) lim = min(lim, t_lo);
                 if (lane == 0)
                 {
-                    tail_ahead = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(SW_OWN + 1, SW_EP | (g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!(help_delay & (4u << 16)))
+                        tail_ahead = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!(help_delay & (2u << 16)))
+                        __hip_atomic_store(SW_OWN + 1, SW_EP | (g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if (g >= lim) g = n_groups;  // a helper's
             }
@@ -3322,13 +3324,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     };
     // tests: workgroup 0 starts its list help_delay us late, so that the
     // others run out first and help it (MI_CRC32C_SORT_HELP_DELAY_US)
-    if (help_delay && blockIdx.x == 0)
+    if ((help_delay & 0xFFFFu) && blockIdx.x == 0)
     {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < uint64_t(help_delay) * 100u) __builtin_amdgcn_s_sleep(8);
+        while (__builtin_amdgcn_s_memrealtime() - t0 < uint64_t(help_delay & 0xFFFFu) * 100u)
+            __builtin_amdgcn_s_sleep(8);
     }
     groups(std::integral_constant<bool, false>{});
-    if (helpable)
+    if (helpable && !(help_delay & (1u << 16)))
         while (claim()) groups(std::integral_constant<bool, true>{});
     SORT_STAMP(5);
     lane_items();
