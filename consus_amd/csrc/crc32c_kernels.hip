@@ -1905,9 +1905,13 @@ constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
 // Entries (one 128-B line) between two workgroups' record-indexed regions
 // of the descriptor list: no line is shared by two regions (round 6, help).
 constexpr uint32_t kSortPad = 8;
-// A helper takes a range from another workgroup's list only while it has at
-// least this many groups left beyond the owner's grab count.
+// A helper takes a range from another workgroup's list only while at least
+// this many of its help-zone groups are unreserved.
 constexpr uint32_t kHelpMin = 2;
+// The owner reserves its own help-zone groups this many at a time.
+constexpr uint32_t kHelpChunk = 16;
+// Help word of a workgroup: epoch (16 bits) | tail (24) | front (24).
+constexpr uint64_t kHelpMask = 0xFFFFFF;
 
 // A 16-B write-through (sc1) store: visible to other XCDs once the storing
 // wave's vmcnt has drained (MI355X_MICROARCH.md, inter-workgroup visibility).
@@ -2068,6 +2072,9 @@ struct SortShared
     uint32_t next_fin;         // finish-pass records taken
     uint32_t n_multi;          // items of split records in this share (none: it may be helped)
     uint32_t help[kBlock / 64][2];  // per wave, helping: the next and the end group of its range
+    uint32_t res_end;          // help zone: the owner's groups reserved so far end here
+    uint32_t res_final;        // ... and its last reservation ended them here (~0: not yet)
+    uint32_t res_busy;         // a wave is reserving
     uint32_t lane_base;        // the first lane item's position among the last pieces
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
@@ -2645,8 +2652,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // descriptors write-through (sc1; nt stores are not, MI355X_MICROARCH.md
     // inter-workgroup visibility) for the helpers' sc1 loads.
     bool helpable = false;
-    auto put = [&](uint4* dst, const uint4& dv) {
-        if (helpable && !(help_delay & (8u << 16)))
+    uint32_t wt_from = ~0u;  // list positions from here on are written through (the help zone)
+    auto put = [&](uint4* dst, const uint4& dv, uint32_t pos) {
+        if (pos >= wt_from)
             store16_sc1(dst, dv);
         else
             __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
@@ -2660,11 +2668,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint32_t stage_nf = 0;
     auto put_full = [&](uint32_t pos, const uint4& dv) {
         if (staged) stage_lds[pos] = dv;
-        else put(fullv + S.full_base + pos, dv);
+        else put(fullv + S.full_base + pos, dv, pos);
     };
     auto put_last = [&](uint32_t pos, const uint4& dv) {
         if (staged) stage_lds[stage_nf + pos] = dv;
-        else put(lastv + pos, dv);
+        else put(lastv + pos, dv, stage_nf + pos);
     };
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
         for (uint32_t i = 0; i < f.nf; ++i) put_full(fpos + i, desc(r, a, L, f, f.klo + i));
@@ -2748,6 +2756,18 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     staged = n_items <= kLdsBytes / 16;
     helpable = epoch != 0 && S.n_multi == 0;
+    // The help zone: the last zone/8 of the groups (the smallest), which
+    // helpers may take; the owner takes the rest without reservations.
+    const uint32_t hz_groups = (n_full + S.lane_base + 7) / 8;
+    const uint32_t zone8 = (help_delay >> 20) & 15u ? (help_delay >> 20) & 15u : 3u;
+    const uint32_t s0 = helpable ? hz_groups - min(hz_groups, hz_groups * zone8 / 8) : hz_groups;
+    if (helpable && !(help_delay & (8u << 16))) wt_from = 8 * s0;
+    if (threadIdx.x == 0)
+    {
+        S.res_end = s0;
+        S.res_final = helpable ? ~0u : hz_groups;
+        S.res_busy = 0;
+    }
     stage_nf = n_full;
     if (n_items)
     {
@@ -2778,7 +2798,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     {
         // list order out: full pieces to their region, the rest after rlo
         for (uint32_t i = threadIdx.x; i < n_items; i += kBlock)
-            put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
+            put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i], i);
         __syncthreads();
     }
     stage_tables(tables);  // ends with a barrier; every thread's descriptor stores are done
@@ -2788,19 +2808,22 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 
     // (4) Groups of 8 team items, largest first, one LDS grab per group.
     const uint32_t n_groups = (n_long + 7) / 8;
-    // Help (round 6): a workgroup whose team groups are done takes groups
-    // from the END of another's list.  Every write of a helped group is
-    // idempotent -- a whole record's CRC, finished in the loop -- so a group
-    // done by both the owner and a helper is only wasted work, never wrong;
-    // a share with split records (whose pieces XOR into out[]) is never
-    // helped.  Per workgroup, in steal_ws (agent-scope words, this launch's
-    // epoch in the high half): [0] tail -- groups at or past it belong to
-    // helpers, lowered by their CAS; [1] the owner's grab count; [2] rlo and
-    // n_long of its list.  The owner's waves read the tail at each grab (the
-    // load issued one grab ahead) and stop at it; its finish pass covers the
-    // groups below the tail it reads after its team groups.
+    // Help (round 6): a workgroup whose own team groups are done takes groups
+    // from the END of another's list, inside that list's help zone (its last
+    // zone/8 groups, the smallest; their descriptors are written through,
+    // sc1, for the helpers' sc0 sc1 loads from other XCDs).  One word per
+    // workgroup in steal_ws: epoch (16 bits) | tail (24) | front (24).  The
+    // owner takes its groups below the zone freely (LDS counter) and its zone
+    // groups kHelpChunk at a time by one agent-scope add to the front; a
+    // helper takes a quarter of [front, tail) from the tail by CAS, never
+    // below the front.  So every group is hashed exactly once: the owner's
+    // are [0, res_final), the helpers' [res_final, n_groups), and the
+    // owner's finish pass covers its own.  A helped group's records are
+    // finished in the loop (out[] only).  Shares with split records (whose
+    // pieces XOR into out[]) neither help nor are helped.  [2]: rlo + pad
+    // and n_long of the list.
 #define SW_OWN (steal_ws + 4 * blockIdx.x)
-#define SW_EP (uint64_t(epoch) << 32)
+#define SW_EP (uint64_t(epoch & 0xFFFFu) << 48)
     if (epoch && threadIdx.x == 0)
     {
         uint64_t* const sw_own = SW_OWN;
@@ -2808,7 +2831,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         __hip_atomic_store(sw_own + 2, (uint64_t(rlo) + pad) | (uint64_t(n_long) << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(sw_own, ep | (helpable ? n_groups : 0u), __ATOMIC_RELAXED,
+        // front = s0, tail = n_groups: the help zone, nothing reserved yet
+        __hip_atomic_store(sw_own, ep | (helpable ? (uint64_t(n_groups) << 24) | s0 : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint32_t tl = threadIdx.x & (kTeam - 1);
@@ -2852,8 +2876,27 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // helped list, which has no full pieces either, needs no other base).
     const uint4* srcL = lastv - n_full;
     uint32_t src_long = n_long, src_groups = n_groups;
-    uint32_t lim = n_groups;         // own list: groups from the tail on are the helpers'
-    uint64_t tail_ahead = SW_EP | n_groups;  // lane 0: the tail word, loaded a grab ahead
+    // The owner's help-zone groups, reserved kHelpChunk at a time from the
+    // front of its word by one agent-scope add (helpers take theirs from the
+    // tail by CAS, never below the front): every group is done exactly once.
+    auto reserve = [&]() {
+        if (lane == 0 && atomicCAS(&S.res_busy, 0u, 1u) == 0u)
+        {
+            const uint64_t old = __hip_atomic_fetch_add(SW_OWN, uint64_t(kHelpChunk), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t f = uint32_t(old & kHelpMask), t = uint32_t((old >> 24) & kHelpMask);
+            if (f >= t)
+                S.res_final = S.res_end;
+            else
+            {
+                const uint32_t ne = min(f + kHelpChunk, t);
+                S.res_end = ne;
+                if (ne >= t) S.res_final = ne;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            S.res_busy = 0;
+        }
+    };
     // (5) Lane items, 64 per grab, one per lane (lane
     // items).  A lane hashes the 16-B aligned blocks its item touches with
     // the slice-by-16 tables: bytes before the item are zeroed (leading zeros
@@ -2973,28 +3016,26 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             d = d1;
         }
     };
-    // Help (round 6): the widest remaining range of another workgroup's list
-    // (tail - grab count), a quarter of it taken from its end by one CAS on
-    // its tail word; false when none has kHelpMin groups left.
+    // Help (round 6): the widest unreserved help zone of another workgroup
+    // (tail - front), a quarter of it taken from its end by one CAS on its
+    // word; false when none has kHelpMin groups left.
     auto claim = [&]() -> bool {
-        for (int tries = 0; tries < 16; ++tries)
+        const uint64_t ep16 = epoch & 0xFFFFu;
+        for (int tries = 0; tries < 4; ++tries)
         {
-            uint32_t best = 0, bv = 0, bprog = 0;
+            uint32_t best = 0, bv = 0;
             for (uint32_t v0 = 0; v0 < gridDim.x; v0 += 64)
             {
                 const uint32_t v = v0 + lane;
                 if (v < gridDim.x && v != blockIdx.x)
                 {
-                    const uint64_t t = __hip_atomic_load(steal_ws + 4 * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t pr = __hip_atomic_load(steal_ws + 4 * v + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // no grab of this launch yet: progress 0 (a late workgroup)
-                    const uint32_t pg = (pr >> 32) == epoch ? uint32_t(pr) : 0u;
-                    const uint32_t rem = (t >> 32) == epoch && uint32_t(t) > pg ? uint32_t(t) - pg : 0u;
+                    const uint64_t w = __hip_atomic_load(steal_ws + 4 * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t f = uint32_t(w & kHelpMask), t = uint32_t((w >> 24) & kHelpMask);
+                    const uint32_t rem = (w >> 48) == ep16 && t > f ? t - f : 0u;
                     if (rem > best)
                     {
                         best = rem;
                         bv = v;
-                        bprog = pg;
                     }
                 }
             }
@@ -3003,12 +3044,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             {
                 const uint32_t ob = uint32_t(__shfl_xor(int(best), dd));
                 const uint32_t ov = uint32_t(__shfl_xor(int(bv), dd));
-                const uint32_t op = uint32_t(__shfl_xor(int(bprog), dd));
                 if (ob > best || (ob == best && ov < bv))
                 {
                     best = ob;
                     bv = ov;
-                    bprog = op;
                 }
             }
             if (best < kHelpMin) return false;
@@ -3017,12 +3056,13 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             {
                 uint64_t* const w = steal_ws + 4 * bv;
                 uint64_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                while ((old >> 32) == epoch && uint32_t(old) > bprog + 1)
+                for (;;)
                 {
-                    const uint32_t t = uint32_t(old);
-                    const uint32_t k = max(1u, (t - bprog) / 4);
-                    if (__hip_atomic_compare_exchange_strong(w, &old, old - k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT))
+                    const uint32_t f = uint32_t(old & kHelpMask), t = uint32_t((old >> 24) & kHelpMask);
+                    if ((old >> 48) != ep16 || t < f + kHelpMin) break;
+                    const uint32_t k = max(1u, (t - f) / 4);  // a quarter: many helpers share a victim
+                    if (__hip_atomic_compare_exchange_strong(w, &old, old - (uint64_t(k) << 24), __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     {
                         lo = t - k;
                         hi = t;
@@ -3069,22 +3109,21 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             uint32_t g = 0;
             if (lane == 0) g = atomicAdd(&S.next_group, 1u);
             g = uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
-            if (helpable)
+            if (!helpable || g < s0) return g;
+            // the help zone: only groups below the reserved end are ours
+            for (;;)
             {
-                // a word of an earlier launch (this launch's not yet stored) is ignored
-                const uint32_t t_ep = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(tail_ahead >> 32))));
-                const uint32_t t_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(tail_ahead))));
-                if (t_ep == epoch) lim = min(lim, t_lo);
-                if (lane == 0)
+                const uint32_t e = uint32_t(__builtin_amdgcn_readfirstlane(int(__hip_atomic_load(&S.res_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))));
+                if (g < e)
                 {
-                    if (!(help_delay & (4u << 16)))
-                        tail_ahead = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!(help_delay & (2u << 16)))
-                        __hip_atomic_store(SW_OWN + 1, SW_EP | (g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (g + kHelpChunk / 2 == e) reserve();  // the next chunk, before it is needed
+                    return g;
                 }
-                if (g >= lim) g = n_groups;  // a helper's
+                if (g >= uint32_t(__builtin_amdgcn_readfirstlane(int(__hip_atomic_load(&S.res_final, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))))
+                    return n_groups;
+                reserve();
+                __builtin_amdgcn_s_sleep(1);
             }
-            return g;
         };
         auto load_desc = [&](uint32_t g) {
             const uint32_t i = g * 8 + tw;
@@ -3358,11 +3397,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // whole records in groups at or past the tail were helped (finished by
     // their helpers); every group below it was done here (round 6)
     uint32_t n_whole = S.lane_base;  // n_long - n_full
-    if (helpable)
-    {
-        const uint64_t t = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((t >> 32) == epoch) n_whole = min(n_whole, 8u * uint32_t(t));
-    }
+    if (helpable) n_whole = min(n_whole, 8u * S.res_final);  // the helpers' groups start there
     const uint4* const dl = lastv;
     for (;;)
     {
@@ -3402,11 +3437,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // whole records in groups at or past the tail were helped (finished by
     // their helpers); every group below it was done here (round 6)
     uint32_t n_whole = S.lane_base;  // n_long - n_full
-    if (helpable)
-    {
-        const uint64_t t = __hip_atomic_load(SW_OWN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((t >> 32) == epoch) n_whole = min(n_whole, 8u * uint32_t(t));
-    }
+    if (helpable) n_whole = min(n_whole, 8u * S.res_final);  // the helpers' groups start there
     const uint4* const dl = lastv;
     for (uint32_t k0 = threadIdx.x; k0 < n_whole; k0 += FU * kBlock)
     {

@@ -762,7 +762,8 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
                        sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base,
                        epoch ? c->srt_steal.as<uint64_t>() : nullptr, epoch, 0};
     if (const char* e = std::getenv("MI_CRC32C_SORT_HELP_DELAY_US")) ws.help_delay = uint32_t(std::atoi(e)) & 0xFFFFu;
-    // A/B bits (dev): 1 no help taken, 2 no progress stores, 4 no tail loads, 8 nt descriptors
+    // A/B bits (dev): 1 no help taken, 8 no write-through descriptors; bits 4-7:
+    // the help zone in eighths of the groups (0: the default, 3)
     if (const char* e = std::getenv("MI_CRC32C_SORT_HELP_DBG")) ws.help_delay |= uint32_t(std::atoi(e)) << 16;
     // MI_CRC32C_SORT_BARRIER_SKEW=1 (tests): the kernel waits for one arrival
     // more than the grid has, so every workgroup's wait times out

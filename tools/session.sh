@@ -73,7 +73,7 @@ while [ $# -gt 0 ]; do
               MI_CRC32C_SORT_HELP=$h timeout -k 10 120 python3 tools/mid_probe.py --mib ${MID_MIB:-64,128,256,512} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }
               grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd help=$h /"
             done; done | tee -a "$OUT/helpab.out" ;;
-    helpdbg) for rnd in 1 2; do for cfg in ${HELPDBG_CFGS:-"0 0" "1 0" "1 1" "1 3" "1 7" "1 15" "1 8" "1 2" "1 4"}; do
+    helpdbg) for rnd in 1 2; do for cfg in ${HELPDBG_CFGS:-"0 0" "1 0" "1 1" "1 9" "1 32" "1 80" "1 16"}; do
               set -- $cfg
               r=$(MI_CRC32C_SORT_HELP=$1 MI_CRC32C_SORT_HELP_DBG=$2 timeout -k 10 120 python3 tools/zipf_probe.py 2>&1 | tail -1) || { echo "$r"; exit 1; }
               echo "round $rnd help=$1 dbg=$2 $r"; case "$r" in *MISMATCH*) exit 1;; esac
