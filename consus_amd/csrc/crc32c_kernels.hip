@@ -2766,7 +2766,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     {
         S.res_end = s0;
         S.res_final = helpable ? ~0u : hz_groups;
-        S.res_busy = 0;
+        // busy until this launch's word is stored (below): no reservation may
+        // add to the last launch's word
+        S.res_busy = helpable ? 1u : 0u;
     }
     stage_nf = n_full;
     if (n_items)
@@ -2834,6 +2836,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         // front = s0, tail = n_groups: the help zone, nothing reserved yet
         __hip_atomic_store(sw_own, ep | (helpable ? (uint64_t(n_groups) << 24) | s0 : 0u), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+        if (helpable)
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stored before any reservation adds to it
+            __hip_atomic_store(&S.res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t tw = lane / kTeam;

@@ -753,7 +753,8 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
     if (sorted_help())
     {
         if ((st = reserve_zeroed(c->srt_steal, size_t(grid) * 32, c->stream))) return st;
-        if (++c->steal_epoch == 0) c->steal_epoch = 1;
+        // the kernel keeps 16 bits of it; 0 is never an epoch (zeroed words)
+        c->steal_epoch = c->steal_epoch % 65535u + 1u;
         epoch = c->steal_epoch;
     }
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
