@@ -2490,6 +2490,8 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 // where each workgroup ran: HW_ID (cu, sh, se fields) and XCC_ID (round 6)
 __device__ uint32_t g_sort_hw[256 * 2];
+// workgroup 0's fold values by list position, and s0 / res_end / res_final (help debugging)
+__device__ uint32_t g_sort_dbg[8192 + 8];
 #define SORT_STAMP(k)                                                                        \
     do                                                                                       \
     {                                                                                        \
@@ -2759,7 +2761,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // The help zone: the last zone/8 of the groups (the smallest), which
     // helpers may take; the owner takes the rest without reservations.
     const uint32_t hz_groups = (n_full + S.lane_base + 7) / 8;
-    const uint32_t zone8 = (help_delay >> 20) & 15u ? (help_delay >> 20) & 15u : 3u;
+    const uint32_t zone8 = (help_delay >> 20) & 15u ? ((help_delay >> 20) & 15u) % 9u : 3u;  // 9: none
     const uint32_t s0 = helpable ? hz_groups - min(hz_groups, hz_groups * zone8 / 8) : hz_groups;
     if (helpable && !(help_delay & (8u << 16))) wt_from = 8 * s0;
     if (threadIdx.x == 0)
@@ -3314,6 +3316,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                 if (!INLOOP && !helping)
                 {
                     if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
+#if MI_SORT_STAMP
+                if (tl == 0 && cur.recf != kSortNone && !multi && blockIdx.x == 0 &&
+                    cur.slot - uint32_t(rlo + pad) < 8192u)
+                    g_sort_dbg[cur.slot - uint32_t(rlo + pad)] = W;
+#endif
                 }
                 else if (cur.recf != kSortNone && !multi)
                 {
@@ -3382,6 +3389,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     SORT_STAMP(5);
     lane_items();
     SORT_STAMP(6);
+#if MI_SORT_STAMP
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+    {
+        g_sort_dbg[8192] = s0;
+        g_sort_dbg[8193] = S.res_end;
+        g_sort_dbg[8194] = S.res_final;
+        g_sort_dbg[8195] = n_groups;
+        g_sort_dbg[8196] = S.lane_base;
+        g_sort_dbg[8197] = helpable;
+    }
+#endif
     if (INLOOP) return;  // whole records were finished in the loop
     // Finish pass, in list order (round 5): a whole record's fold value W
     // (wr at its slot, eight consecutive words per group) is Z_m(raw) of its
@@ -3482,6 +3500,11 @@ extern "C" __attribute__((visibility("default"))) int mi_debug_sort_stamps(uint6
 {
     n = n < sizeof(g_sort_stamp) / 8 ? n : sizeof(g_sort_stamp) / 8;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_stamp), n * 8) == hipSuccess ? 0 : -5;
+}
+extern "C" __attribute__((visibility("default"))) int mi_debug_sort_dbg(uint32_t* host, size_t n)
+{
+    n = n < sizeof(g_sort_dbg) / 4 ? n : sizeof(g_sort_dbg) / 4;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_dbg), n * 4) == hipSuccess ? 0 : -5;
 }
 extern "C" __attribute__((visibility("default"))) int mi_debug_sort_hw(uint32_t* host, size_t n)
 {

@@ -78,7 +78,7 @@ while [ $# -gt 0 ]; do
               r=$(MI_CRC32C_SORT_HELP=$1 MI_CRC32C_SORT_HELP_DBG=$2 timeout -k 10 120 python3 tools/zipf_probe.py 2>&1 | tail -1) || { echo "$r"; exit 1; }
               echo "round $rnd help=$1 dbg=$2 $r"; case "$r" in *MISMATCH*) exit 1;; esac
             done; done | tee "$OUT/helpdbg.out" ;;
-    helpdebug) run help_debug 300 python3 -u tools/help_debug.py && cat "$OUT/help_debug.out" ;;
+    helpdebug) run help_debug 300 python3 -u tools/help_debug.py ${HELPDBG_LIB:-} && cat "$OUT/help_debug.out" ;;
     sortedtests) run pytest_sorted 900 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py tests/test_gpu_errors.py -x -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
