@@ -2824,25 +2824,29 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // are [0, res_final), the helpers' [res_final, n_groups), and the
     // owner's finish pass covers its own.  A helped group's records are
     // finished in the loop (out[] only).  Shares with split records (whose
-    // pieces XOR into out[]) neither help nor are helped.  [2]: rlo + pad
-    // and n_long of the list.
+    // pieces XOR into out[]) neither help nor are helped.  [1]: rlo + pad
+    // and n_long of the list; [2]: the launch's epoch once [0] and [1] are
+    // set (the flag helpers poll).
 #define SW_OWN (steal_ws + 4 * blockIdx.x)
 #define SW_EP (uint64_t(epoch & 0xFFFFu) << 48)
     if (epoch && threadIdx.x == 0)
     {
         uint64_t* const sw_own = SW_OWN;
-        const uint64_t ep = SW_EP;
-        __hip_atomic_store(sw_own + 2, (uint64_t(rlo) + pad) | (uint64_t(n_long) << 32), __ATOMIC_RELAXED,
+        // (a) the word, by an atomic exchange: atomics execute at the memory
+        // side, and a plain or sc1 store could land after the first
+        // reservation's add (measured: reservations then added to the last
+        // launch's word).  front = s0, tail = n_groups: nothing reserved yet.
+        (void)__hip_atomic_exchange(sw_own, SW_EP | (helpable ? (uint64_t(n_groups) << 24) | s0 : 0u),
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (b) the list's place, then the flag helpers poll (MI355X_MICROARCH.md
+        // valid hand-off: sc1 payload -- the zone descriptors above and this
+        // word -- drained, then an sc1 flag store; the helpers poll it with
+        // sc1 loads and read the payload with sc1 loads)
+        __hip_atomic_store(sw_own + 1, (uint64_t(rlo) + pad) | (uint64_t(n_long) << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // front = s0, tail = n_groups: the help zone, nothing reserved yet
-        __hip_atomic_store(sw_own, ep | (helpable ? (uint64_t(n_groups) << 24) | s0 : 0u), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        if (helpable)
-        {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stored before any reservation adds to it
-            __hip_atomic_store(&S.res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        __hip_atomic_store(sw_own + 2, uint64_t(epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (helpable) __hip_atomic_store(&S.res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t tw = lane / kTeam;
@@ -3036,9 +3040,13 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             for (uint32_t v0 = 0; v0 < gridDim.x; v0 += 64)
             {
                 const uint32_t v = v0 + lane;
-                if (v < gridDim.x && v != blockIdx.x)
+                if (v < gridDim.x && v != blockIdx.x &&
+                    __hip_atomic_load(steal_ws + 4 * v + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch)
                 {
-                    const uint64_t w = __hip_atomic_load(steal_ws + 4 * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // the word itself by an atomic (memory side): an L2 copy
+                    // from an earlier scan would be stale
+                    const uint64_t w = __hip_atomic_fetch_or(steal_ws + 4 * v, uint64_t(0), __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t f = uint32_t(w & kHelpMask), t = uint32_t((w >> 24) & kHelpMask);
                     const uint32_t rem = (w >> 48) == ep16 && t > f ? t - f : 0u;
                     if (rem > best)
@@ -3064,7 +3072,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             if (lane == 0)
             {
                 uint64_t* const w = steal_ws + 4 * bv;
-                uint64_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint64_t old = __hip_atomic_fetch_or(w, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 for (;;)
                 {
                     const uint32_t f = uint32_t(old & kHelpMask), t = uint32_t((old >> 24) & kHelpMask);
@@ -3085,7 +3093,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             {
                 // groups helped, all launches (mi_debug_sort_helped; tests)
                 if (lane == 0) __hip_atomic_fetch_add(ctrl + 6, hi - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t m = __hip_atomic_load(steal_ws + 4 * bv + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t m = __hip_atomic_load(steal_ws + 4 * bv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t m_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(m))));
                 src_long = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(m >> 32))));
                 srcL = items + m_lo;
