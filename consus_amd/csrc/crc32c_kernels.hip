@@ -2893,21 +2893,27 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // front of its word by one agent-scope add (helpers take theirs from the
     // tail by CAS, never below the front): every group is done exactly once.
     auto reserve = [&]() {
-        if (lane == 0 && atomicCAS(&S.res_busy, 0u, 1u) == 0u)
+        uint32_t busy = 0;
+        if (lane == 0 &&
+            __hip_atomic_compare_exchange_strong(&S.res_busy, &busy, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
         {
             const uint64_t old = __hip_atomic_fetch_add(SW_OWN, uint64_t(kHelpChunk), __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t f = uint32_t(old & kHelpMask), t = uint32_t((old >> 24) & kHelpMask);
+            // atomic reads and writes of the shared state: a plain read here was
+            // served from a copy loaded before the lock (another wave had
+            // reserved meanwhile), and ended the list early
+            const uint32_t cur = __hip_atomic_load(&S.res_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (f >= t)
-                S.res_final = S.res_end;
+                __hip_atomic_store(&S.res_final, cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             else
             {
                 const uint32_t ne = min(f + kHelpChunk, t);
-                S.res_end = ne;
-                if (ne >= t) S.res_final = ne;
+                __hip_atomic_store(&S.res_end, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (ne >= t) __hip_atomic_store(&S.res_final, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            S.res_busy = 0;
+            __hip_atomic_store(&S.res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     };
     // (5) Lane items, 64 per grab, one per lane (lane
