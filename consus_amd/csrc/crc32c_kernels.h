@@ -145,12 +145,6 @@ struct SortedWorkspace
     // ctrl[32] counts arrivals, bar_base = its value before this launch.
     int fused;
     uint32_t bar_base;
-    // Help across workgroups (round 6): 4 words per workgroup, zero at first
-    // use; steal_epoch != 0 (a new value per launch on this workspace) turns
-    // it on, 0 off.
-    uint64_t* steal;
-    uint32_t steal_epoch;
-    uint32_t help_delay;  // tests: workgroup 0 starts its list this many us late
 };
 constexpr uint64_t kSortedMaxCount = 1ull << 30;
 uint32_t sorted_blocks(uint64_t count);

@@ -1902,23 +1902,6 @@ constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a s
 constexpr uint32_t kSortFirst = 0x40000000u;  // ... its first piece (carries the init)
 constexpr uint32_t kSortRecMask = 0x3FFFFFFFu;
 constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
-// Entries (one 128-B line) between two workgroups' record-indexed regions
-// of the descriptor list: no line is shared by two regions (round 6, help).
-constexpr uint32_t kSortPad = 8;
-// A helper takes a range from another workgroup's list only while at least
-// this many of its help-zone groups are unreserved.
-constexpr uint32_t kHelpMin = 2;
-// The owner reserves its own help-zone groups this many at a time.
-constexpr uint32_t kHelpChunk = 16;
-// Help word of a workgroup: epoch (16 bits) | tail (24) | front (24).
-constexpr uint64_t kHelpMask = 0xFFFFFF;
-
-// A 16-B write-through (sc1) store: visible to other XCDs once the storing
-// wave's vmcnt has drained (MI355X_MICROARCH.md, inter-workgroup visibility).
-__device__ __forceinline__ void store16_sc1(void* p, const uint4& v)
-{
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(make_u32x4(v)) : "memory");
-}
 
 uint32_t sorted_blocks(uint64_t count) { return uint32_t((count + kSortRecs - 1) / kSortRecs); }
 
@@ -2070,11 +2053,6 @@ struct SortShared
     uint32_t next_lane;        // lane items taken (64 per grab)
     uint32_t teams_done;       // waves whose team groups are done (finish overlap)
     uint32_t next_fin;         // finish-pass records taken
-    uint32_t n_multi;          // items of split records in this share (none: it may be helped)
-    uint32_t help[kBlock / 64][2];  // per wave, helping: the next and the end group of its range
-    uint32_t res_end;          // help zone: the owner's groups reserved so far end here
-    uint32_t res_final;        // ... and its last reservation ended them here (~0: not yet)
-    uint32_t res_busy;         // a wave is reserving
     uint32_t lane_base;        // the first lane item's position among the last pieces
     uint32_t bound[4];         // (record, piece) of the first item and of the end
     uint32_t blk[2];           // cost blocks holding the two targets (nb: none)
@@ -2490,8 +2468,6 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 // where each workgroup ran: HW_ID (cu, sh, se fields) and XCC_ID (round 6)
 __device__ uint32_t g_sort_hw[256 * 2];
-// workgroup 0's fold values by list position, and s0 / res_end / res_final (help debugging)
-__device__ uint32_t g_sort_dbg[8192 + 8];
 #define SORT_STAMP(k)                                                                        \
     do                                                                                       \
     {                                                                                        \
@@ -2513,8 +2489,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint64_t* __restrict__ blk_cost, uint32_t nb, uint32_t* __restrict__ ctrl,
     uint4* __restrict__ items, uint64_t item_cap, uint32_t* __restrict__ wr, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2, uint32_t plog,
-    uint32_t lrows, int fused, uint32_t bar_base, uint64_t* __restrict__ steal_ws, uint32_t epoch,
-    uint32_t help_delay)
+    uint32_t lrows, int fused, uint32_t bar_base)
 {
     SortShared& S = *reinterpret_cast<SortShared*>(smem + kLdsBytes);
     const uint64_t piece = uint64_t(1) << plog;
@@ -2526,7 +2501,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     if (threadIdx.x == 0) S.next_lane = 0;
     if (threadIdx.x == 0) S.teams_done = 0;
     if (threadIdx.x == 0) S.next_fin = 0;
-    if (threadIdx.x == 0) S.n_multi = 0;
     // small batches finish each whole record right after its fold (below):
     // Z_{-128} is staged with the tables
     // whole records finished in the loop (RB = 4, small batches) or by the
@@ -2637,29 +2611,15 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         return make_uint4(uint32_t(ps), uint32_t(ps >> 32), uint32_t(pe - ps),
                           uint32_t(r) | (f.s.n > 1 ? kSortMulti : 0u) | (head ? kSortFirst : 0u));
     };
-    // Workgroup b's record-indexed slots start 8 b entries (a 128-B line) past
-    // rlo, so no line of descriptors (or fold values) is shared by two
-    // workgroups' regions: a helping workgroup on another XCD reads a
-    // region's lines and must never hold a stale copy of one in its L2
-    // (round 6, helpers).  The full pieces' regions follow all of them.
-    const uint64_t pad = uint64_t(kSortPad) * blockIdx.x;
-    uint4* const fullv = items + count + uint64_t(kSortPad) * gridDim.x;
-    uint4* const lastv = items + rlo + pad;
+    uint4* const fullv = items + count;
+    uint4* const lastv = items + rlo;
     // absolute slots: full run at fpos, last piece at lpos
     // Descriptors go out with non-temporal stores: the ~2 MB of them per XCD
     // then do not sit dirty in the XCD's 4 MB L2 through the hash phase
     // (measured: prologue 8 us longer, step 8-10 us shorter).  The group loop
     // reads them two groups ahead (non-temporal loads there: neutral).
-    // A share that other workgroups may help with (round 6) writes its
-    // descriptors write-through (sc1; nt stores are not, MI355X_MICROARCH.md
-    // inter-workgroup visibility) for the helpers' sc1 loads.
-    bool helpable = false;
-    uint32_t wt_from = ~0u;  // list positions from here on are written through (the help zone)
-    auto put = [&](uint4* dst, const uint4& dv, uint32_t pos) {
-        if (pos >= wt_from)
-            store16_sc1(dst, dv);
-        else
-            __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
+    auto put = [&](uint4* dst, const uint4& dv) {
+        __builtin_nontemporal_store(make_u32x4(dv), reinterpret_cast<u32x4_t*>(dst));
     };
     // Up to kLdsBytes / 16 items, the descriptors go to LDS at their list
     // position (the table image's space: the tables are staged after), and
@@ -2670,11 +2630,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint32_t stage_nf = 0;
     auto put_full = [&](uint32_t pos, const uint4& dv) {
         if (staged) stage_lds[pos] = dv;
-        else put(fullv + S.full_base + pos, dv, pos);
+        else put(fullv + S.full_base + pos, dv);
     };
     auto put_last = [&](uint32_t pos, const uint4& dv) {
         if (staged) stage_lds[stage_nf + pos] = dv;
-        else put(lastv + pos, dv, stage_nf + pos);
+        else put(lastv + pos, dv);
     };
     auto place = [&](uint64_t r, uint64_t a, uint32_t L, const RecInfo& f, uint32_t fpos, uint32_t lpos) {
         for (uint32_t i = 0; i < f.nf; ++i) put_full(fpos + i, desc(r, a, L, f, f.klo + i));
@@ -2703,7 +2663,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                 const RecInfo f = info(r, av[u], Lv[u]);
                 uint32_t rf, rl;
                 take(f, rf, rl);
-                if (!second && f.s.n > 1 && (f.nf || f.last)) S.n_multi = 1u;  // a split record's items
                 if (second)
                     place(r, av[u], Lv[u], f, rf, rl);  // the bins hold cursors now
                 else if (held)
@@ -2740,7 +2699,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             const uint32_t fb = uint32_t(blockIdx.x * fpw);
             S.n_full = nf;
             S.n_items = nf + uint32_t(total);
-            if (nf > fpw || count + uint64_t(gridDim.x) * (fpw + kSortPad) > item_cap)
+            if (nf > fpw || count + uint64_t(gridDim.x) * fpw > item_cap)
             {
                 ctrl[1] = 1;  // workspace too small (understated total_bytes): out[] left alone
                 ctrl[2] = 1;  // sticky: an asynchronous batch's is reported at the next stream sync
@@ -2757,21 +2716,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     __syncthreads();
     const uint32_t n_items = S.n_items, n_full = S.n_full;
     staged = n_items <= kLdsBytes / 16;
-    helpable = epoch != 0 && S.n_multi == 0;
-    // The help zone: the last zone/8 of the groups (the smallest), which
-    // helpers may take; the owner takes the rest without reservations.
-    const uint32_t hz_groups = (n_full + S.lane_base + 7) / 8;
-    const uint32_t zone8 = (help_delay >> 20) & 15u ? ((help_delay >> 20) & 15u) % 9u : 3u;  // 9: none
-    const uint32_t s0 = helpable ? hz_groups - min(hz_groups, hz_groups * zone8 / 8) : hz_groups;
-    if (helpable && !(help_delay & (8u << 16))) wt_from = 8 * s0;
-    if (threadIdx.x == 0)
-    {
-        S.res_end = s0;
-        S.res_final = helpable ? ~0u : hz_groups;
-        // busy until this launch's word is stored (below): no reservation may
-        // add to the last launch's word
-        S.res_busy = helpable ? 1u : 0u;
-    }
     stage_nf = n_full;
     if (n_items)
     {
@@ -2802,52 +2746,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     {
         // list order out: full pieces to their region, the rest after rlo
         for (uint32_t i = threadIdx.x; i < n_items; i += kBlock)
-            put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i], i);
+            put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
         __syncthreads();
     }
-    stage_tables(tables);  // ends with a barrier; every thread's descriptor stores are done
+    stage_tables(tables);  // ends with a barrier
     SORT_STAMP(4);
     // team items first, lane items (positions n_long ..) after them
     const uint32_t n_long = n_full + S.lane_base;
 
     // (4) Groups of 8 team items, largest first, one LDS grab per group.
     const uint32_t n_groups = (n_long + 7) / 8;
-    // Help (round 6): a workgroup whose own team groups are done takes groups
-    // from the END of another's list, inside that list's help zone (its last
-    // zone/8 groups, the smallest; their descriptors are written through,
-    // sc1, for the helpers' sc0 sc1 loads from other XCDs).  One word per
-    // workgroup in steal_ws: epoch (16 bits) | tail (24) | front (24).  The
-    // owner takes its groups below the zone freely (LDS counter) and its zone
-    // groups kHelpChunk at a time by one agent-scope add to the front; a
-    // helper takes a quarter of [front, tail) from the tail by CAS, never
-    // below the front.  So every group is hashed exactly once: the owner's
-    // are [0, res_final), the helpers' [res_final, n_groups), and the
-    // owner's finish pass covers its own.  A helped group's records are
-    // finished in the loop (out[] only).  Shares with split records (whose
-    // pieces XOR into out[]) neither help nor are helped.  [1]: rlo + pad
-    // and n_long of the list; [2]: the launch's epoch once [0] and [1] are
-    // set (the flag helpers poll).
-#define SW_OWN (steal_ws + 4 * blockIdx.x)
-#define SW_EP (uint64_t(epoch & 0xFFFFu) << 48)
-    if (epoch && threadIdx.x == 0)
-    {
-        uint64_t* const sw_own = SW_OWN;
-        // (a) the word, by an atomic exchange: atomics execute at the memory
-        // side, and a plain or sc1 store could land after the first
-        // reservation's add (measured: reservations then added to the last
-        // launch's word).  front = s0, tail = n_groups: nothing reserved yet.
-        (void)__hip_atomic_exchange(sw_own, SW_EP | (helpable ? (uint64_t(n_groups) << 24) | s0 : 0u),
-                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // (b) the list's place, then the flag helpers poll (MI355X_MICROARCH.md
-        // valid hand-off: sc1 payload -- the zone descriptors above and this
-        // word -- drained, then an sc1 flag store; the helpers poll it with
-        // sc1 loads and read the payload with sc1 loads)
-        __hip_atomic_store(sw_own + 1, (uint64_t(rlo) + pad) | (uint64_t(n_long) << 32), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(sw_own + 2, uint64_t(epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (helpable) __hip_atomic_store(&S.res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
     const uint32_t tl = threadIdx.x & (kTeam - 1);
     const uint32_t tw = lane / kTeam;
     const uint32_t li = lane_info();
@@ -2880,42 +2788,56 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
-    const uint4* const listF = fullv + S.full_base;  // full pieces first
-    // The list the group loop runs (wave-uniform): this workgroup's own (full
-    // pieces at listF, the rest from srcL), then, helping, ranges of other
-    // workgroups' lists (no full pieces).  One set of registers for both:
-    // the own list's values are restored for the lane items and the finish.
-    // Only a workgroup without split records helps (its n_full is 0, so a
-    // helped list, which has no full pieces either, needs no other base).
-    const uint4* srcL = lastv - n_full;
-    uint32_t src_long = n_long, src_groups = n_groups;
-    // The owner's help-zone groups, reserved kHelpChunk at a time from the
-    // front of its word by one agent-scope add (helpers take theirs from the
-    // tail by CAS, never below the front): every group is done exactly once.
-    auto reserve = [&]() {
-        uint32_t busy = 0;
-        if (lane == 0 &&
-            __hip_atomic_compare_exchange_strong(&S.res_busy, &busy, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
-        {
-            const uint64_t old = __hip_atomic_fetch_add(SW_OWN, uint64_t(kHelpChunk), __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t f = uint32_t(old & kHelpMask), t = uint32_t((old >> 24) & kHelpMask);
-            // atomic reads and writes of the shared state: a plain read here was
-            // served from a copy loaded before the lock (another wave had
-            // reserved meanwhile), and ended the list early
-            const uint32_t cur = __hip_atomic_load(&S.res_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (f >= t)
-                __hip_atomic_store(&S.res_final, cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-            {
-                const uint32_t ne = min(f + kHelpChunk, t);
-                __hip_atomic_store(&S.res_end, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (ne >= t) __hip_atomic_store(&S.res_final, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            __hip_atomic_store(&S.res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+    auto grab = [&]() {
+        uint32_t g = 0;
+        if (lane == 0) g = atomicAdd(&S.next_group, 1u);
+        return uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
     };
+    const uint4* const listF = items + count + S.full_base;  // full pieces first
+    const uint4* const listL = items + rlo - n_full;          // then the rest
+    auto load_desc = [&](uint32_t g) {
+        const uint32_t i = g * 8 + tw;
+        const uint4* p = (g < n_groups && i < n_long) ? (i < n_full ? listF : listL) + i
+                                                       : reinterpret_cast<const uint4*>(zero16);
+        return *p;
+    };
+    // Uniform shape of a group: n rows (its largest item, padded to an even
+    // count with a leading zero row), the first row of that item, the last
+    // row in which some team's item starts (or its init word spills into),
+    // and the first row from which every lane reads item bytes (n: never, in
+    // a group with teams but no item).  The list is descending except where
+    // the 512-row full pieces meet the 513-row whole records (the full
+    // pieces are listed first), so the largest and smallest item are taken
+    // over the group's teams, not from its first and last.
+    struct Shape
+    {
+        int32_t n, fmin, fedge, fast;
+    };
+    auto shape_of = [&](const uint4& d, uint32_t g) {
+        Shape s{0, 0, 0, 0};
+        if (g >= n_groups) return s;
+        const uint32_t tlast = min(7u, n_long - 1 - g * 8);
+        const int rv = int(sort_rows(d));
+        int32_t rmax = 0, rmin = int32_t(kSortRows);
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+        {
+            const int32_t x = __builtin_amdgcn_readlane(rv, int(t * kTeam));
+            rmax = t <= tlast ? max(rmax, x) : rmax;
+            rmin = t <= tlast ? min(rmin, x) : rmin;
+        }
+        s.n = (rmax + RB - 1) & ~(RB - 1);
+        s.fmin = s.n - rmax;
+        s.fedge = s.n - rmin + 1;
+        s.fast = tlast == 7 ? s.fedge + 1 : s.n;
+        return s;
+    };
+    auto row_ptr = [&](const SortView& v, int32_t r, bool fast) {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(v.p0 + uint64_t(uint32_t(r)) * kRowBytes);
+        if (!fast) p = (r >= v.lo && r <= v.hi) ? p : zero16;
+        return p;
+    };
+
     // (5) Lane items, 64 per grab, one per lane (lane
     // items).  A lane hashes the 16-B aligned blocks its item touches with
     // the slice-by-16 tables: bytes before the item are zeroed (leading zeros
@@ -2929,10 +2851,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // longer item takes another round)
     constexpr int32_t kLaneBlocks = MI_SORT_LANE_BLOCKS;
     auto lane_items = [&]() {
-        // the own list's lane items (re-read: the group loop's registers held
-        // helped lists meanwhile)
-        const uint32_t n_lane = S.n_items - (S.n_full + S.lane_base);
-        const uint4* const listLane = lastv + S.lane_base;
+        const uint32_t n_lane = n_items - n_long;
+        const uint4* const listLane = listL + n_long;
         auto grab64 = [&]() {
             uint32_t c = 0;
             if (lane == 0) c = atomicAdd(&S.next_lane, 64u);
@@ -3035,385 +2955,182 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             d = d1;
         }
     };
-    // Help (round 6): the widest unreserved help zone of another workgroup
-    // (tail - front), a quarter of it taken from its end by one CAS on its
-    // word; false when none has kHelpMin groups left.
-    auto claim = [&]() -> bool {
-        const uint64_t ep16 = epoch & 0xFFFFu;
-        for (int tries = 0; tries < 4; ++tries)
-        {
-            uint32_t best = 0, bv = 0;
-            for (uint32_t v0 = 0; v0 < gridDim.x; v0 += 64)
-            {
-                const uint32_t v = v0 + lane;
-                if (v < gridDim.x && v != blockIdx.x &&
-                    __hip_atomic_load(steal_ws + 4 * v + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch)
-                {
-                    // the word itself by an atomic (memory side): an L2 copy
-                    // from an earlier scan would be stale
-                    const uint64_t w = __hip_atomic_fetch_or(steal_ws + 4 * v, uint64_t(0), __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t f = uint32_t(w & kHelpMask), t = uint32_t((w >> 24) & kHelpMask);
-                    const uint32_t rem = (w >> 48) == ep16 && t > f ? t - f : 0u;
-                    if (rem > best)
-                    {
-                        best = rem;
-                        bv = v;
-                    }
-                }
-            }
+    uint32_t g_cur = grab();
+    uint4 d_cur = load_desc(g_cur);
+    uint32_t g_nxt = grab();
+    uint4 d_nxt = load_desc(g_nxt);
+    Shape shA = shape_of(d_cur, g_cur);
+    SortView vA = sort_view(d_cur, shA.n, tl, inits, ones_word);
+    const uint32_t slot0 = rlo - n_full + tw;  // slot of list position i: slot0 + 8 g (whole records)
+    vA.slot = slot0 + g_cur * 8;
+    Shape shB{0, 0, 0, 0};
+    SortView vB = vA;
+    const SortView& cur0 = vA;
+    // Row ring of RB buffers: row r of a group sits in b[r % RB]; each row
+    // step issues row r + RB - 1 (this group's, or one of the next group's
+    // first rows) before folding row r.  Groups are padded to a multiple of
+    // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
+    // flight per wave while another folds (measured on the headline batch:
+    // one row ahead costs < 1 % against three; here it keeps the padding to
+    // half a row per group).  RB = 4 serves small batches (pieces below
+    // 64 KiB), where a wave has only a group or two of up to 33 rows, so the
+    // rows in flight per wave, not the HBM, bound it; it finishes whole
+    // records in the loop (no finish pass).  RB = 8 (128 VGPRs once the
+    // finish pass is gone) measured no faster than 4 at 1 MiB - 2 GiB
+    // (round 4, profiles/r04_sorted_ring_sweep.txt).
+    uint4 b[RB];
 #pragma unroll
-            for (int dd = 32; dd >= 1; dd >>= 1)
+    for (int j = 0; j < RB - 1; ++j) b[j] = load16_edge(row_ptr(cur0, j, false));
+    if (RB == 2 && shA.n == 2) b[1] = load16_edge(row_ptr(cur0, 1, false));
+    __builtin_amdgcn_sched_barrier(0);
+    // One group: hash `cur` (shape sh) while the next group's view is built
+    // into `nxt`.  The loop runs it twice per iteration with the two views
+    // swapped (round 2 A/B: profiles/r02_sorted_view32_pingpong_ab.txt), so the ~20 registers of a view are never
+    // copied at the back edge.
+    auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
+        // A 2-row group runs no body loop: its row 1 was issued at the end of
+        // the previous step, into b[1] once that step's last row was folded
+        // (see below), a whole fold, finish and group header ahead.
+        const bool pre = RB == 2 && sh.n == 2;
+        const uint32_t g_nn = grab();
+        const uint4 d_nn = load_desc(g_nn);
+        shn = shape_of(d_nxt, g_nxt);
+        nxt = sort_view(d_nxt, shn.n, tl, inits, ones_word);
+        nxt.slot = slot0 + g_nxt * 8;
+        uint32_t V[4] = {0, 0, 0, 0};
+        const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
+        // General row: padding skip, start mask and init word (rows up to
+        // fedge), end mask (row n - 1), zero-block reads.  Used for the first
+        // rows and the last RB of a group; the rows between take the body
+        // loop below: all lanes read item bytes, nothing to mask.
+        auto gen_row = [&](uint4 d, int32_t r) {
+            if (r < fmin) return;  // the padding row: V stays 0
+            if (r <= fedge)
             {
-                const uint32_t ob = uint32_t(__shfl_xor(int(best), dd));
-                const uint32_t ov = uint32_t(__shfl_xor(int(bv), dd));
-                if (ob > best || (ob == best && ov < bv))
-                {
-                    best = ob;
-                    bv = ov;
-                }
+                // row f: (d & keep) ^ ~init in one v_bitop3 per dword (truth
+                // table index S0 S1 S2 = d keep x, MSB first: 0x6A)
+                const bool at_f = r == cur.f;
+                d.x = at_f ? __builtin_amdgcn_bitop3_b32(d.x, cur.kf.x, cur.xf.x, 0x6A) : d.x;
+                d.y = at_f ? __builtin_amdgcn_bitop3_b32(d.y, cur.kf.y, cur.xf.y, 0x6A) : d.y;
+                d.z = at_f ? __builtin_amdgcn_bitop3_b32(d.z, cur.kf.z, cur.xf.z, 0x6A) : d.z;
+                d.w = at_f ? __builtin_amdgcn_bitop3_b32(d.w, cur.kf.w, cur.xf.w, 0x6A) : d.w;
+                d.x ^= r == cur.f + 1 ? cur.xs : 0u;
             }
-            if (best < kHelpMin) return false;
-            uint32_t lo = 0, hi = 0;
-            if (lane == 0)
+            if (r == n - 1)
             {
-                uint64_t* const w = steal_ws + 4 * bv;
-                uint64_t old = __hip_atomic_fetch_or(w, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (;;)
-                {
-                    const uint32_t f = uint32_t(old & kHelpMask), t = uint32_t((old >> 24) & kHelpMask);
-                    if ((old >> 48) != ep16 || t < f + kHelpMin) break;
-                    const uint32_t k = max(1u, (t - f) / 4);  // a quarter: many helpers share a victim
-                    if (__hip_atomic_compare_exchange_strong(w, &old, old - (uint64_t(k) << 24), __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    {
-                        lo = t - k;
-                        hi = t;
-                        break;
-                    }
-                }
+                d.x &= cur.ke.x;
+                d.y &= cur.ke.y;
+                d.z &= cur.ke.z;
+                d.w &= cur.ke.w;
             }
-            lo = uint32_t(__builtin_amdgcn_readfirstlane(int(lo)));
-            hi = uint32_t(__builtin_amdgcn_readfirstlane(int(hi)));
-            if (hi > lo)
-            {
-                // groups helped, all launches (mi_debug_sort_helped; tests)
-                if (lane == 0) __hip_atomic_fetch_add(ctrl + 6, hi - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t m = __hip_atomic_load(steal_ws + 4 * bv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t m_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(m))));
-                src_long = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(m >> 32))));
-                srcL = items + m_lo;
-                src_groups = (src_long + 7) / 8;
-                if (lane == 0)
-                {
-                    S.help[threadIdx.x >> 6][0] = lo;
-                    S.help[threadIdx.x >> 6][1] = hi;
-                }
-                return true;
-            }
-        }
-        return false;
-    };
-    // The group loop, instantiated twice: the own list (HELP false), and a
-    // range of another workgroup's list (HELP true: sc0 sc1 descriptor loads,
-    // every record finished in the loop, the range from LDS).  Two copies of
-    // the code, but neither carries the other's state in its registers.
-    auto groups = [&](auto help_tag) {
-        constexpr bool helping = decltype(help_tag)::value;
-        auto grab = [&]() {
-            if (helping)
-            {
-                // this wave's helped range, kept in LDS (no registers across the loop)
-                const uint32_t hn = S.help[threadIdx.x >> 6][0], he = S.help[threadIdx.x >> 6][1];
-                if (hn >= he) return src_groups;
-                if (lane == 0) S.help[threadIdx.x >> 6][0] = hn + 1;
-                return uint32_t(__builtin_amdgcn_readfirstlane(int(hn)));
-            }
-            uint32_t g = 0;
-            if (lane == 0) g = atomicAdd(&S.next_group, 1u);
-            g = uint32_t(__builtin_amdgcn_readfirstlane(int(g)));
-            if (!helpable || g < s0) return g;
-            // the help zone: only groups below the reserved end are ours
-            for (;;)
-            {
-                const uint32_t e = uint32_t(__builtin_amdgcn_readfirstlane(int(__hip_atomic_load(&S.res_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))));
-                if (g < e)
-                {
-                    if (g + kHelpChunk / 2 == e) reserve();  // the next chunk, before it is needed
-                    return g;
-                }
-                if (g >= uint32_t(__builtin_amdgcn_readfirstlane(int(__hip_atomic_load(&S.res_final, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))))
-                    return n_groups;
-                reserve();
-                __builtin_amdgcn_s_sleep(1);
-            }
+            if (r == fmin)
+                row_first(V, d);  // the largest item starts here; every other team's row is zero
+            else
+                row_update(V, d, li);
         };
-        auto load_desc = [&](uint32_t g) {
-            const uint32_t i = g * 8 + tw;
-            const bool in = g < src_groups && i < src_long;
-            const uint4* p = in ? (i < n_full ? listF : srcL) + i : reinterpret_cast<const uint4*>(zero16);
-            if (helping)
-            {
-                // another workgroup's list, stored sc1 this launch: a volatile
-                // (sc0 sc1) load, never served from a stale line of this L1/L2
-                typedef const volatile __attribute__((address_space(1))) u32x4_t* vgptr;
-                const u32x4_t v = *(vgptr)(uintptr_t)p;
-                return make_uint4(v.x, v.y, v.z, v.w);
-            }
-            return *p;
-        };
-        // Uniform shape of a group: n rows (its largest item, padded to an even
-        // count with a leading zero row), the first row of that item, the last
-        // row in which some team's item starts (or its init word spills into),
-        // and the first row from which every lane reads item bytes (n: never, in
-        // a group with teams but no item).  The list is descending except where
-        // the 512-row full pieces meet the 513-row whole records (the full
-        // pieces are listed first), so the largest and smallest item are taken
-        // over the group's teams, not from its first and last.
-        struct Shape
+        // body rows [hend, n - RB): after every team's first row and init
+        // word (full groups only: a partial group has teams without items)
+        const int32_t hend = fast < n ? min(n - RB, (fedge + RB) & ~(RB - 1)) : n - RB;
+        int32_t r = 0;
+        for (; r < hend; r += RB)
         {
-            int32_t n, fmin, fedge, fast;
-        };
-        auto shape_of = [&](const uint4& d, uint32_t g) {
-            Shape s{0, 0, 0, 0};
-            if (g >= src_groups) return s;
-            const uint32_t tlast = min(7u, src_long - 1 - g * 8);
-            const int rv = int(sort_rows(d));
-            int32_t rmax = 0, rmin = int32_t(kSortRows);
-    #pragma unroll
-            for (uint32_t t = 0; t < 8; ++t)
-            {
-                const int32_t x = __builtin_amdgcn_readlane(rv, int(t * kTeam));
-                rmax = t <= tlast ? max(rmax, x) : rmax;
-                rmin = t <= tlast ? min(rmin, x) : rmin;
-            }
-            s.n = (rmax + RB - 1) & ~(RB - 1);
-            s.fmin = s.n - rmax;
-            s.fedge = s.n - rmin + 1;
-            s.fast = tlast == 7 ? s.fedge + 1 : s.n;
-            return s;
-        };
-        auto row_ptr = [&](const SortView& v, int32_t r, bool fast) {
-            const uint8_t* p = reinterpret_cast<const uint8_t*>(v.p0 + uint64_t(uint32_t(r)) * kRowBytes);
-            if (!fast) p = (r >= v.lo && r <= v.hi) ? p : zero16;
-            return p;
-        };
-
-        const uint32_t slot0 = uint32_t(rlo + pad) - n_full + tw;  // slot of list position i: slot0 + 8 g (whole records)
-        uint32_t g_nxt;
-        uint4 d_nxt;
-        Shape shA, shB;
-        SortView vA, vB;
-        // Row ring of RB buffers: row r of a group sits in b[r % RB]; each row
-        // step issues row r + RB - 1 (this group's, or one of the next group's
-        // first rows) before folding row r.  Groups are padded to a multiple of
-        // RB rows, so the roles never change.  RB = 2 (kSortRing): one row in
-        // flight per wave while another folds (measured on the headline batch:
-        // one row ahead costs < 1 % against three; here it keeps the padding to
-        // half a row per group).  RB = 4 serves small batches (pieces below
-        // 64 KiB), where a wave has only a group or two of up to 33 rows, so the
-        // rows in flight per wave, not the HBM, bound it; it finishes whole
-        // records in the loop (no finish pass).  RB = 8 (128 VGPRs once the
-        // finish pass is gone) measured no faster than 4 at 1 MiB - 2 GiB
-        // (round 4, profiles/r04_sorted_ring_sweep.txt).
-        uint4 b[RB];
-        // the first two groups of a list, the ring's first rows
-        auto prime = [&]() {
-            const uint32_t g_cur = grab();
-            const uint4 d_cur = load_desc(g_cur);
-            g_nxt = grab();
-            d_nxt = load_desc(g_nxt);
-            shA = shape_of(d_cur, g_cur);
-            vA = sort_view(d_cur, shA.n, tl, inits, ones_word);
-            vA.slot = slot0 + g_cur * 8;
-            shB = Shape{0, 0, 0, 0};
-            vB = vA;
-    #pragma unroll
-            for (int j = 0; j < RB - 1; ++j) b[j] = load16_edge(row_ptr(vA, j, false));
-            if (RB == 2 && shA.n == 2) b[1] = load16_edge(row_ptr(vA, 1, false));
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        // One group: hash `cur` (shape sh) while the next group's view is built
-        // into `nxt`.  The loop runs it twice per iteration with the two views
-        // swapped (round 2 A/B: profiles/r02_sorted_view32_pingpong_ab.txt), so the ~20 registers of a view are never
-        // copied at the back edge.
-        auto step = [&](const SortView& cur, const Shape& sh, SortView& nxt, Shape& shn) {
-            // A 2-row group runs no body loop: its row 1 was issued at the end of
-            // the previous step, into b[1] once that step's last row was folded
-            // (see below), a whole fold, finish and group header ahead.
-            const bool pre = RB == 2 && sh.n == 2;
-            const uint32_t g_nn = grab();
-            const uint4 d_nn = load_desc(g_nn);
-            shn = shape_of(d_nxt, g_nxt);
-            nxt = sort_view(d_nxt, shn.n, tl, inits, ones_word);
-            nxt.slot = slot0 + g_nxt * 8;
-            uint32_t V[4] = {0, 0, 0, 0};
-            const int32_t n = sh.n, fmin = sh.fmin, fedge = sh.fedge, fast = sh.fast;
-            // General row: padding skip, start mask and init word (rows up to
-            // fedge), end mask (row n - 1), zero-block reads.  Used for the first
-            // rows and the last RB of a group; the rows between take the body
-            // loop below: all lanes read item bytes, nothing to mask.
-            auto gen_row = [&](uint4 d, int32_t r) {
-                if (r < fmin) return;  // the padding row: V stays 0
-                if (r <= fedge)
-                {
-                    // row f: (d & keep) ^ ~init in one v_bitop3 per dword (truth
-                    // table index S0 S1 S2 = d keep x, MSB first: 0x6A)
-                    const bool at_f = r == cur.f;
-                    d.x = at_f ? __builtin_amdgcn_bitop3_b32(d.x, cur.kf.x, cur.xf.x, 0x6A) : d.x;
-                    d.y = at_f ? __builtin_amdgcn_bitop3_b32(d.y, cur.kf.y, cur.xf.y, 0x6A) : d.y;
-                    d.z = at_f ? __builtin_amdgcn_bitop3_b32(d.z, cur.kf.z, cur.xf.z, 0x6A) : d.z;
-                    d.w = at_f ? __builtin_amdgcn_bitop3_b32(d.w, cur.kf.w, cur.xf.w, 0x6A) : d.w;
-                    d.x ^= r == cur.f + 1 ? cur.xs : 0u;
-                }
-                if (r == n - 1)
-                {
-                    d.x &= cur.ke.x;
-                    d.y &= cur.ke.y;
-                    d.z &= cur.ke.z;
-                    d.w &= cur.ke.w;
-                }
-                if (r == fmin)
-                    row_first(V, d);  // the largest item starts here; every other team's row is zero
-                else
-                    row_update(V, d, li);
-            };
-            // body rows [hend, n - RB): after every team's first row and init
-            // word (full groups only: a partial group has teams without items)
-            const int32_t hend = fast < n ? min(n - RB, (fedge + RB) & ~(RB - 1)) : n - RB;
-            int32_t r = 0;
-            for (; r < hend; r += RB)
-            {
-    #pragma unroll
-                for (int j = 0; j < RB; ++j)
-                {
-                    {
-                        const int32_t rr = r + j + RB - 1;
-                        const uint8_t* pp = row_ptr(cur, rr, false);
-                        b[(j + RB - 1) % RB] = rr <= fedge ? load16_edge(pp) : load16(pp);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    gen_row(b[j], r + j);
-                }
-            }
-            {
-                const uint8_t* pr = reinterpret_cast<const uint8_t*>(cur.p0);
-                for (; r < n - RB; r += RB)
-                {
-    #pragma unroll
-                    for (int j = 0; j < RB; ++j)
-                    {
-                        b[(j + RB - 1) % RB] = load16(pr + uint32_t(r + j + RB - 1) * uint32_t(kRowBytes));
-                        __builtin_amdgcn_sched_barrier(0);
-                        row_update(V, b[j], li);
-                    }
-                }
-            }
-            // the last RB rows: row n - 1, then the next group's first rows
-    #pragma unroll
+#pragma unroll
             for (int j = 0; j < RB; ++j)
             {
-                if (!(j == 0 && pre))
-                    b[(j + RB - 1) % RB] = load16_edge(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
+                {
+                    const int32_t rr = r + j + RB - 1;
+                    const uint8_t* pp = row_ptr(cur, rr, false);
+                    b[(j + RB - 1) % RB] = rr <= fedge ? load16_edge(pp) : load16(pp);
+                }
                 __builtin_amdgcn_sched_barrier(0);
-                gen_row(b[j], n - RB + j);
+                gen_row(b[j], r + j);
             }
-            // the next group's row 1 if it has two rows (b[1] is free now)
-            if (RB == 2 && shn.n == 2) b[1] = load16_edge(row_ptr(nxt, 1, false));
-            const uint32_t W = team_fold(V);
-            flush();  // the previous group's split-record pieces
+        }
+        {
+            const uint8_t* pr = reinterpret_cast<const uint8_t*>(cur.p0);
+            for (; r < n - RB; r += RB)
             {
-                const bool multi = cur.recf != kSortNone && (cur.recf & kSortMulti);
-                // whole records: the fold value by slot, eight consecutive words per
-                // group (stores to out[rec] here hit a line per record, scattered:
-                // 8-11 us of the configs[2] step, profiles/r03_sorted_late_finish_ab.txt)
-                if (!INLOOP && !helping)
+#pragma unroll
+                for (int j = 0; j < RB; ++j)
                 {
-                    if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
-#if MI_SORT_STAMP
-                if (tl == 0 && cur.recf != kSortNone && !multi && blockIdx.x == 0 &&
-                    cur.slot - uint32_t(rlo + pad) < 8192u)
-                    g_sort_dbg[cur.slot - uint32_t(rlo + pad)] = W;
-#endif
+                    b[(j + RB - 1) % RB] = load16(pr + uint32_t(r + j + RB - 1) * uint32_t(kRowBytes));
+                    __builtin_amdgcn_sched_barrier(0);
+                    row_update(V, b[j], li);
                 }
-                else if (cur.recf != kSortNone && !multi)
-                {
-                    // small batches (RB >= 4): a wave has a group or two, so the
-                    // finish pass's two dependent global reads per record cost
-                    // more than finishing here: crc = ~Z_{-m}(W) from LDS tables.
-                    // A helped group (another workgroup's) is finished here too.
-                    const uint32_t m = cur.m & 127u, nn = 128u - m;
-                    uint32_t t = zT_n(W, nn & 15u);
-                    t = (nn & 16u) ? zT<4>(t) : t;
-                    t = (nn & 32u) ? zG(kLdsZ32, t) : t;
-                    t = (nn & 64u) ? zG(kLdsZ64, t) : t;
-                    t = zG(kLdsZInv, t);
-                    if (tl == 0) out[cur.recf & kSortRecMask] = ~(m ? t : W);
-                }
-                p_multi = __builtin_amdgcn_ballot_w64(multi) != 0;
-                if (p_multi)
-                {
-                    // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
-                    const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
-                    const uint32_t q = tl & 3u;
-                    uint32_t pz_new = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
-                    // an opaque definition: without it the loop-carried copy of pz at
-                    // the loop header waited for this load every group
-                    asm volatile("" : "+v"(pz_new));
-                    pz = pz_new;
-                }
-                p_recf = multi ? cur.recf : kSortNone;
-                p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;
             }
-            g_nxt = g_nn;
-            d_nxt = d_nn;
-        };
-        // twice per iteration with the two views swapped: the ~20 registers of a
-        // view are never copied at the back edge (~60 v_mov per group before)
-        prime();
-        while (shA.n > 0)
-        {
-            step(vA, shA, vB, shB);
-            if (shB.n <= 0) break;
-            step(vB, shB, vA, shA);
         }
-        flush();
-#if MI_SORT_FIN_OVERLAP
-        // this wave's fold values (wr) are stored: count it done for the
-        // finish pass, which starts when every wave's team groups are, beside
-        // the other waves' lane items (and help)
-        if (!helping)
+        // the last RB rows: row n - 1, then the next group's first rows
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
         {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) atomicAdd(&S.teams_done, 1u);
+            if (!(j == 0 && pre))
+                b[(j + RB - 1) % RB] = load16_edge(j == 0 ? row_ptr(cur, n - 1, false) : row_ptr(nxt, j - 1, false));
+            __builtin_amdgcn_sched_barrier(0);
+            gen_row(b[j], n - RB + j);
         }
-#endif
+        // the next group's row 1 if it has two rows (b[1] is free now)
+        if (RB == 2 && shn.n == 2) b[1] = load16_edge(row_ptr(nxt, 1, false));
+        const uint32_t W = team_fold(V);
+        flush();  // the previous group's split-record pieces
+        {
+            const bool multi = cur.recf != kSortNone && (cur.recf & kSortMulti);
+            // whole records: the fold value by slot, eight consecutive words per
+            // group (stores to out[rec] here hit a line per record, scattered:
+            // 8-11 us of the configs[2] step, profiles/r03_sorted_late_finish_ab.txt)
+            if (!INLOOP)
+            {
+                if (tl == 0 && cur.recf != kSortNone && !multi) wr[cur.slot] = W;
+            }
+            else if (cur.recf != kSortNone && !multi)
+            {
+                // small batches (RB >= 4): a wave has a group or two, so the
+                // finish pass's two dependent global reads per record cost
+                // more than finishing here: crc = ~Z_{-m}(W) from LDS tables
+                const uint32_t m = cur.m & 127u, nn = 128u - m;
+                uint32_t t = zT_n(W, nn & 15u);
+                t = (nn & 16u) ? zT<4>(t) : t;
+                t = (nn & 32u) ? zG(kLdsZ32, t) : t;
+                t = (nn & 64u) ? zG(kLdsZ64, t) : t;
+                t = zG(kLdsZInv, t);
+                if (tl == 0) out[cur.recf & kSortRecMask] = ~(m ? t : W);
+            }
+            p_multi = __builtin_amdgcn_ballot_w64(multi) != 0;
+            if (p_multi)
+            {
+                // fold value from the team's lane 0 to lanes 0..3 (quad_perm [0,0,0,0])
+                const uint32_t Wq = uint32_t(__builtin_amdgcn_mov_dpp(int(W), 0x00, 0xF, 0xF, false));
+                const uint32_t q = tl & 3u;
+                uint32_t pz_new = zneg[(cur.m & 127u) * 1024u + q * 256u + ((Wq >> (8 * q)) & 0xFFu)];
+                // an opaque definition: without it the loop-carried copy of pz at
+                // the loop header waited for this load every group
+                asm volatile("" : "+v"(pz_new));
+                pz = pz_new;
+            }
+            p_recf = multi ? cur.recf : kSortNone;
+            p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;
+        }
+        g_nxt = g_nn;
+        d_nxt = d_nn;
     };
-    // tests: workgroup 0 starts its list help_delay us late, so that the
-    // others run out first and help it (MI_CRC32C_SORT_HELP_DELAY_US)
-    if ((help_delay & 0xFFFFu) && blockIdx.x == 0)
+    // twice per iteration with the two views swapped: the ~20 registers of a
+    // view are never copied at the back edge (~60 v_mov per group before)
+    while (shA.n > 0)
     {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < uint64_t(help_delay & 0xFFFFu) * 100u)
-            __builtin_amdgcn_s_sleep(8);
+        step(vA, shA, vB, shB);
+        if (shB.n <= 0) break;
+        step(vB, shB, vA, shA);
     }
-    groups(std::integral_constant<bool, false>{});
-    if (helpable && !(help_delay & (1u << 16)))
-        while (claim()) groups(std::integral_constant<bool, true>{});
+    flush();
+#if MI_SORT_FIN_OVERLAP
+    // this wave's fold values (wr) are stored: count it done for the finish
+    // pass, which starts when every wave's team groups are, beside the other
+    // waves' lane items
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) atomicAdd(&S.teams_done, 1u);
+#endif
     SORT_STAMP(5);
     lane_items();
     SORT_STAMP(6);
-#if MI_SORT_STAMP
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-    {
-        g_sort_dbg[8192] = s0;
-        g_sort_dbg[8193] = S.res_end;
-        g_sort_dbg[8194] = S.res_final;
-        g_sort_dbg[8195] = n_groups;
-        g_sort_dbg[8196] = S.lane_base;
-        g_sort_dbg[8197] = helpable;
-    }
-#endif
     if (INLOOP) return;  // whole records were finished in the loop
     // Finish pass, in list order (round 5): a whole record's fold value W
     // (wr at its slot, eight consecutive words per group) is Z_m(raw) of its
@@ -3433,11 +3150,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         __builtin_amdgcn_s_sleep(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     constexpr uint32_t FU = 4;
-    // whole records in groups at or past the tail were helped (finished by
-    // their helpers); every group below it was done here (round 6)
-    uint32_t n_whole = S.lane_base;  // n_long - n_full
-    if (helpable) n_whole = min(n_whole, 8u * S.res_final);  // the helpers' groups start there
-    const uint4* const dl = lastv;
+    const uint32_t n_whole = n_long - n_full;
+    const uint4* const dl = items + rlo;
     for (;;)
     {
         uint32_t c0 = 0;
@@ -3451,7 +3165,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             const uint32_t k = c0 + u * 64 + lane;
             dv[u] = k < n_whole ? dl[k] : make_uint4(0, 0, 0, kSortMulti);
-            wv[u] = k < n_whole ? wr[uint64_t(rlo) + pad + k] : 0u;
+            wv[u] = k < n_whole ? wr[uint64_t(rlo) + k] : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
@@ -3473,11 +3187,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     __syncthreads();  // the workgroup's own stores are visible to it past the barrier
     constexpr uint32_t FU = 4;
-    // whole records in groups at or past the tail were helped (finished by
-    // their helpers); every group below it was done here (round 6)
-    uint32_t n_whole = S.lane_base;  // n_long - n_full
-    if (helpable) n_whole = min(n_whole, 8u * S.res_final);  // the helpers' groups start there
-    const uint4* const dl = lastv;
+    const uint32_t n_whole = n_long - n_full;
+    const uint4* const dl = items + rlo;
     for (uint32_t k0 = threadIdx.x; k0 < n_whole; k0 += FU * kBlock)
     {
         uint4 dv[FU];
@@ -3487,7 +3198,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             const uint32_t k = k0 + u * kBlock;
             dv[u] = k < n_whole ? dl[k] : make_uint4(0, 0, 0, kSortMulti);
-            wv[u] = k < n_whole ? wr[uint64_t(rlo) + pad + k] : 0u;
+            wv[u] = k < n_whole ? wr[uint64_t(rlo) + k] : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
@@ -3514,11 +3225,6 @@ extern "C" __attribute__((visibility("default"))) int mi_debug_sort_stamps(uint6
 {
     n = n < sizeof(g_sort_stamp) / 8 ? n : sizeof(g_sort_stamp) / 8;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_stamp), n * 8) == hipSuccess ? 0 : -5;
-}
-extern "C" __attribute__((visibility("default"))) int mi_debug_sort_dbg(uint32_t* host, size_t n)
-{
-    n = n < sizeof(g_sort_dbg) / 4 ? n : sizeof(g_sort_dbg) / 4;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_dbg), n * 4) == hipSuccess ? 0 : -5;
 }
 extern "C" __attribute__((visibility("default"))) int mi_debug_sort_hw(uint32_t* host, size_t n)
 {
@@ -3556,14 +3262,13 @@ hipError_t launch_sorted(const void* base, const uint64_t* offsets, const uint32
     auto k = ws.ring == 4 ? crc32c_sorted_kernel<4> : crc32c_sorted_kernel<2>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), kLdsSorted, stream, b, offsets, lengths, inits,
                        count, ws.blk_cost, nb, ws.ctrl, ws.items, ws.item_cap, ws.wr, out, tables,
-                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base, ws.steal, ws.steal_epoch,
-                       ws.help_delay);
+                       pow2, ws.plog, ws.lane_rows, ws.fused, ws.bar_base);
     return hipGetLastError();
 }
 
 uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, int grid)
 {
-    return count + uint64_t(grid) * (sorted_full_per_wg(count, total_bytes, plog, grid) + kSortPad);
+    return count + uint64_t(grid) * sorted_full_per_wg(count, total_bytes, plog, grid);
 }
 
 // ---------------------------------------------------------------------------

@@ -334,8 +334,6 @@ struct Ctx
     DevBuf data, off, len, inits, out;  // staging of host batches
     DevBuf items, partial, first_pos, int_pos, last_pos, blk, longs;
     DevBuf srt_cost, srt_ctrl, srt_items;  // sorted path (launch_sorted)
-    DevBuf srt_steal;                      // sorted path: help words, 4 per workgroup (zeroed once)
-    uint32_t steal_epoch = 0;              // the last launch's help epoch on srt_steal
     DevBuf win_acc;                        // window path: acc64[count], acc[count], cnt[count], kept zero
     DevBuf done_ctr;                    // direct kernel's completion counter (DoneSignal)
     uint32_t done_seq = 0;
@@ -432,7 +430,7 @@ struct Ctx
         sorted_users = nullptr;
         for (DevBuf* b : {&data, &off, &len, &inits, &out, &items, &partial, &first_pos, &int_pos,
                           &last_pos, &blk, &longs, &srt_cost,
-                          &srt_ctrl, &srt_items, &srt_steal, &win_acc, &done_ctr})
+                          &srt_ctrl, &srt_items, &win_acc, &done_ctr})
             b->release();
         for (PinBuf* b : {&pin_small, &pin_stage, &pin_out}) b->release();
         for (hipEvent_t* e : {&ev0, &ev1, &done})
@@ -712,16 +710,6 @@ bool fused_ok(DeviceState* d, const Ctx* c, int grid)
     return grid <= d->cus && d->sorted_users.load() == 1;
 }
 
-// Help across workgroups in the sorted kernel (round 6: a workgroup whose team
-// groups are done takes groups from the end of another's list; idempotent
-// writes, so a group done twice is only wasted work).  MI_CRC32C_SORT_HELP=0|1
-// (read per batch; A/B and tests).
-bool sorted_help()
-{
-    const char* e = std::getenv("MI_CRC32C_SORT_HELP");
-    return e && !std::strcmp(e, "1");
-}
-
 // The sorted path (crc32c_kernels.hip, "sorted path"): whole records per team.
 int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, const uint32_t* len,
                const uint32_t* inits, size_t count, uint64_t total_bytes, uint32_t* out)
@@ -747,25 +735,10 @@ int run_sorted(DeviceState* d, Ctx* c, const void* base, const uint64_t* off, co
         c->sorted_users = &d->sorted_users;
         c->sorted_users->fetch_add(1);
     }
-    // help across workgroups (round 6): a new epoch per launch on this
-    // context's words (0 is never an epoch: zeroed words are "no launch")
-    uint32_t epoch = 0;
-    if (sorted_help())
-    {
-        if ((st = reserve_zeroed(c->srt_steal, size_t(grid) * 32, c->stream))) return st;
-        // the kernel keeps 16 bits of it; 0 is never an epoch (zeroed words)
-        c->steal_epoch = c->steal_epoch % 65535u + 1u;
-        epoch = c->steal_epoch;
-    }
     SortedWorkspace ws{c->srt_cost.as<uint64_t>(), c->srt_ctrl.as<uint32_t>(),
                        reinterpret_cast<uint4*>(ib), cap,
                        reinterpret_cast<uint32_t*>(ib + cap * 16), plog, sorted_ring(plog),
-                       sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base,
-                       epoch ? c->srt_steal.as<uint64_t>() : nullptr, epoch, 0};
-    if (const char* e = std::getenv("MI_CRC32C_SORT_HELP_DELAY_US")) ws.help_delay = uint32_t(std::atoi(e)) & 0xFFFFu;
-    // A/B bits (dev): 1 no help taken, 8 no write-through descriptors; bits 4-7:
-    // the help zone in eighths of the groups (0: the default, 3)
-    if (const char* e = std::getenv("MI_CRC32C_SORT_HELP_DBG")) ws.help_delay |= uint32_t(std::atoi(e)) << 16;
+                       sorted_lane_rows(), fused_ok(d, c, grid) ? 1 : 0, c->bar_base};
     // MI_CRC32C_SORT_BARRIER_SKEW=1 (tests): the kernel waits for one arrival
     // more than the grid has, so every workgroup's wait times out
     const char* skew = std::getenv("MI_CRC32C_SORT_BARRIER_SKEW");
@@ -956,20 +929,6 @@ void* mi_crc32c_stream(void)
     int st = 0;
     Ctx* c = thread_ctx(&st);
     return c ? static_cast<void*>(c->stream) : nullptr;
-}
-
-// Test hook: groups of the sorted path helped across workgroups (round 6)
-// by launches on this thread's context so far (ctrl[6]); -1 without one.
-long long mi_debug_sort_helped(void)
-{
-    int st = 0;
-    Ctx* c = thread_ctx(&st);
-    if (!c || !c->srt_ctrl.p) return -1;
-    uint32_t* w = c->pin_small.as<uint32_t>() + 9;
-    if (hipMemcpyAsync(w, c->srt_ctrl.as<uint32_t>() + 6, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return -1;
-    return *w;
 }
 
 int mi_crc32c_stream_sync(void)

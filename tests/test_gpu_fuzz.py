@@ -101,12 +101,7 @@ def test_fuzz_round(engine, oracle, round_):
     plog = [None, "9", "10", "12", "13", "14", "15", "16"][int(rng.integers(0, 8))]
     ring = [None, "2", "4"][int(rng.integers(0, 3))]
     lanes = [None, "0", "1", "3"][int(rng.integers(0, 4))]  # rows of a lane item (default 2)
-    # help across workgroups (round 6), with workgroup 0 started late or not
-    helpd = [None, "0", "100"][int(rng.integers(0, 3))]
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
-    if helpd:
-        os.environ["MI_CRC32C_SORT_HELP"] = "1"
-        os.environ["MI_CRC32C_SORT_HELP_DELAY_US"] = helpd
     if lanes:
         os.environ["MI_CRC32C_SORT_LANE_ROWS"] = lanes
     if ring:
@@ -119,8 +114,7 @@ def test_fuzz_round(engine, oracle, round_):
         before = engine.stats()["sorted_batches"]
         engine.device_batch(data, d_off, d_len, count, d_out, inits=d_ini,
                             total_bytes=max(int(lengths.sum(dtype=np.uint64)), 1))
-        assert np.array_equal(d_out.download(np.uint32, count), want), ("sorted", grid, plog, ring, lanes,
-                                                                       helpd)
+        assert np.array_equal(d_out.download(np.uint32, count), want), ("sorted", grid, plog, ring, lanes)
         assert engine.stats()["sorted_batches"] == before + 1
     finally:
         os.environ.pop("MI_CRC32C_VARPATH", None)
@@ -128,8 +122,6 @@ def test_fuzz_round(engine, oracle, round_):
         os.environ.pop("MI_CRC32C_SORT_PIECE_LOG2", None)
         os.environ.pop("MI_CRC32C_SORT_RING", None)
         os.environ.pop("MI_CRC32C_SORT_LANE_ROWS", None)
-        os.environ.pop("MI_CRC32C_SORT_HELP", None)
-        os.environ.pop("MI_CRC32C_SORT_HELP_DELAY_US", None)
 
     # the window path forced (count < 3000 is inside its record bound), at a
     # random workgroup (one wave, four, one twelve-wave workgroup per CU) and

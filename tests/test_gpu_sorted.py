@@ -25,21 +25,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["auto", "auto-1launch", "auto-ring2", "16", "16-nolane", "auto-help",
-                        "16-help"],
+@pytest.fixture(params=["auto", "auto-1launch", "auto-ring2", "16", "16-nolane"],
                 ids=["piece_auto", "piece_auto_one_launch", "piece_auto_ring2", "piece_64k",
-                     "piece_64k_teams_only", "piece_auto_help", "piece_64k_help"])
+                     "piece_64k_teams_only"])
 def sorted_path(engine, request):
     old = os.environ.get("MI_CRC32C_VARPATH")
     os.environ["MI_CRC32C_VARPATH"] = "sorted"
-    if request.param.endswith("-help"):
-        # help across workgroups, workgroup 0 started 300 us late so that
-        # the others run out of groups first and help it
-        os.environ["MI_CRC32C_SORT_HELP"] = "1"
-        os.environ["MI_CRC32C_SORT_HELP_DELAY_US"] = "300"
-        if request.param.startswith("16"):
-            os.environ["MI_CRC32C_SORT_PIECE_LOG2"] = "16"
-    elif request.param == "auto-1launch":
+    if request.param == "auto-1launch":
         os.environ["MI_CRC32C_SORT_FUSED"] = "1"  # cost blocks + a grid barrier in the hash kernel
     elif request.param == "auto-ring2":
         os.environ["MI_CRC32C_SORT_RING"] = "2"
@@ -54,8 +46,6 @@ def sorted_path(engine, request):
     os.environ.pop("MI_CRC32C_SORT_RING", None)
     os.environ.pop("MI_CRC32C_SORT_LANE_ROWS", None)
     os.environ.pop("MI_CRC32C_SORT_FUSED", None)
-    os.environ.pop("MI_CRC32C_SORT_HELP", None)
-    os.environ.pop("MI_CRC32C_SORT_HELP_DELAY_US", None)
     if old is None:
         del os.environ["MI_CRC32C_VARPATH"]
     else:
@@ -572,61 +562,3 @@ def test_sorted_many_lane_items_small_grids(engine, oracle, grid):
     finally:
         for k in ("MI_CRC32C_VARPATH", "MI_CRC32C_SORTED_GRID", "MI_CRC32C_SORT_FUSED"):
             os.environ.pop(k, None)
-
-
-def _helped(engine):
-    import ctypes as C
-    f = engine.lib().mi_debug_sort_helped
-    f.restype = C.c_longlong
-    return int(f())
-
-
-@pytest.mark.parametrize("plog", ["auto", "16"])
-@pytest.mark.parametrize("with_inits", [False, True])
-def test_sorted_help_takes_groups_and_stays_exact(engine, oracle, plog, with_inits, monkeypatch):
-    """Round 6: workgroups whose own groups are done help others, taking
-    groups from the end of their lists (one CAS on the owner's tail word per
-    range; every write idempotent).  Workgroup 0 starts 300 us late
-    (MI_CRC32C_SORT_HELP_DELAY_US), so the others must help it: the helped
-    count grows, and every CRC matches the oracle -- with the size's own
-    piece (4-row ring, every record finished in the loop) and with 64 KiB
-    pieces (2-row ring: the owner's finish pass covers only the groups below
-    its tail, the helpers finish theirs in the loop)."""
-    monkeypatch.setenv("MI_CRC32C_VARPATH", "sorted")
-    monkeypatch.setenv("MI_CRC32C_SORT_HELP", "1")
-    monkeypatch.setenv("MI_CRC32C_SORT_HELP_DELAY_US", "300")
-    if plog != "auto":
-        monkeypatch.setenv("MI_CRC32C_SORT_PIECE_LOG2", plog)
-    rng = np.random.default_rng(61 + with_inits)
-    lengths = engine.zipf_lengths(0xDA7A5EED, 20000).astype(np.uint32)
-    if plog == "auto":
-        # the size's own piece is 2 KiB here: no record longer than it, so no
-        # share holds a split record (those shares are never helped)
-        lengths = np.minimum(lengths, 2048).astype(np.uint32)
-    offsets, end = _packed(rng, lengths, start=int(rng.integers(0, 128)))
-    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
-    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32) if with_inits else None
-    want = oracle.batch(buf, offsets, lengths, inits)
-    before = _helped(engine)
-    for _ in range(3):
-        got = _device_run(engine, buf, offsets, lengths, inits)
-        assert np.array_equal(got, want)
-    assert _helped(engine) > before
-
-
-def test_sorted_help_skips_shares_with_split_records(engine, oracle, monkeypatch):
-    """A share holding pieces of a split record (whose parts XOR into out[])
-    is never helped; the others still are.  Records of 200 KiB among Zipf
-    records, 4 KiB pieces: exact, with the help on and workgroup 0 late."""
-    monkeypatch.setenv("MI_CRC32C_VARPATH", "sorted")
-    monkeypatch.setenv("MI_CRC32C_SORT_HELP", "1")
-    monkeypatch.setenv("MI_CRC32C_SORT_HELP_DELAY_US", "300")
-    monkeypatch.setenv("MI_CRC32C_SORT_PIECE_LOG2", "12")
-    rng = np.random.default_rng(77)
-    lengths = engine.zipf_lengths(0xDA7A5EED, 12000).astype(np.uint32)
-    lengths[rng.integers(0, lengths.size, 40)] = 200 << 10
-    offsets, end = _packed(rng, lengths, start=3)
-    buf = rng.integers(0, 256, end + 64, dtype=np.uint8)
-    want = oracle.batch(buf, offsets, lengths)
-    for _ in range(2):
-        assert np.array_equal(_device_run(engine, buf, offsets, lengths), want)

@@ -65,20 +65,6 @@ while [ $# -gt 0 ]; do
               rm -rf /dev/shm/dltl; env $envs timeout -k 10 120 ./tools/dlog_bench /dev/shm/dltl 8 ${DLOGTL_PER:-25000} 0 0 > "$OUT/dl.out" 2> "$OUT/dl.err" || { cat "$OUT/dl.err"; rm -rf /dev/shm/dltl; exit 1; }
               echo "round $rnd $eng $(cat "$OUT/dl.out")"
             done; done > "$OUT/dlogtl.out"; rm -rf /dev/shm/dltl; cut -c1-200 "$OUT/dlogtl.out" ;;
-    helpab) for rnd in 1 2 3 4; do for h in 0 1; do
-              r=$(MI_CRC32C_SORT_HELP=$h timeout -k 10 120 python3 tools/zipf_probe.py 2>&1 | tail -1) || { echo "$r"; exit 1; }
-              echo "round $rnd help=$h $r"; case "$r" in *MISMATCH*) exit 1;; esac
-            done; done | tee "$OUT/helpab.out"
-            for rnd in 1 2; do for h in 0 1; do
-              MI_CRC32C_SORT_HELP=$h timeout -k 10 120 python3 tools/mid_probe.py --mib ${MID_MIB:-64,128,256,512} --reps 200 > "$OUT/w.out" 2>&1 || { cat "$OUT/w.out"; exit 1; }
-              grep -v "^path" "$OUT/w.out" | sed "s/^/round $rnd help=$h /"
-            done; done | tee -a "$OUT/helpab.out" ;;
-    helpdbg) for rnd in 1 2; do for cfg in ${HELPDBG_CFGS:-"0 0" "1 0" "1 1" "1 9" "1 32" "1 80" "1 16"}; do
-              set -- $cfg
-              r=$(MI_CRC32C_SORT_HELP=$1 MI_CRC32C_SORT_HELP_DBG=$2 timeout -k 10 120 python3 tools/zipf_probe.py 2>&1 | tail -1) || { echo "$r"; exit 1; }
-              echo "round $rnd help=$1 dbg=$2 $r"; case "$r" in *MISMATCH*) exit 1;; esac
-            done; done | tee "$OUT/helpdbg.out" ;;
-    helpdebug) run help_debug 300 python3 -u tools/help_debug.py ${HELPDBG_LIB:-} && cat "$OUT/help_debug.out" ;;
     sortedtests) run pytest_sorted 900 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py tests/test_gpu_errors.py -x -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
