@@ -73,7 +73,7 @@ uint64_t shard_min(uint64_t arg)
 
 // Single host calls below this many bytes are answered on the CPU (size
 // routing).  Measured on MI355X + EPYC 9575F (tools/route_probe.cc,
-// profiles/r03_route_probe.txt, DESIGN.md section 4.4): a GPU round trip of
+// profiles/r03_route_probe.txt, DESIGN.md section 4.7): a GPU round trip of
 // one host call costs 17 us at 16 B, 21 us at 4 KiB, 117 us at 1 MiB and
 // 154 us at 4 MiB (pageable staging); the CPU path runs at ~13 GiB/s (0.03 us
 // at 16 B, 78 us at 1 MiB, 313 us at 4 MiB).  They cross near 1.7 MiB.

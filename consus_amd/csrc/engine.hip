@@ -683,7 +683,7 @@ int sorted_ring(uint32_t plog)
 }
 
 // Records spanning at most this many 128-B rows are hashed one per lane
-// (lane items, DESIGN.md section 4.7); MI_CRC32C_SORT_LANE_ROWS=0..3
+// (lane items, DESIGN.md section 4.2); MI_CRC32C_SORT_LANE_ROWS=0..3
 // overrides (0: every item takes a team).
 uint32_t sorted_lane_rows()
 {

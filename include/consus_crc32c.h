@@ -114,7 +114,7 @@ void mi_crc32c_stats_reset(void);
  * consus::crc32c and mi_crc32c_buffer on HOST memory with n < gpu_min bytes
  * are answered by the engine's CPU path, without a GPU round trip; larger
  * ones, every batch and every device buffer go to the GPU.  The default is
- * the crossover measured on MI355X (DESIGN.md section 4.4); env
+ * the crossover measured on MI355X (DESIGN.md section 4.7); env
  * MI_CRC32C_GPU_MIN (bytes) overrides it at load, this call at run time
  * (0 = every call on the GPU, as the GPU parity tests run).  Returns the
  * previous value. */

@@ -1,4 +1,4 @@
-"""GPU parity of the direct kernel's two forms (DESIGN.md section 7).
+"""GPU parity of the direct kernel's two forms (DESIGN.md section 4.6).
 
 Host batches of records <= 16 KiB take one launch of crc32c_direct_kernel:
 with the 152 KiB LDS table image (1024-thread workgroups) or, for batches of

@@ -1,4 +1,4 @@
-"""GPU parity of the sorted variable-length path (DESIGN.md section 4.7):
+"""GPU parity of the sorted variable-length path (DESIGN.md section 4.2):
 one team per whole record, records binned by row count inside each
 workgroup's cost-balanced share, split records XORed together from their
 pieces.  The piece is sized by the batch (engine.hip sorted_piece_log2: 2 KiB

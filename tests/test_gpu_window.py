@@ -1,5 +1,5 @@
 """GPU parity of the window path (crc32c_kernels.hip "window path", DESIGN.md
-section 4.9): mid-size device batches (at most kWinMaxCount = 8192 records,
+section 4.3): mid-size device batches (at most kWinMaxCount = 8192 records,
 26 MiB by default) in one launch.  Each record is cut into windows of 4, 8
 or 16 rows (512 B - 2 KiB, by batch size) counted back from its end, one
 window per team; a record over several waves is combined through one 64-bit

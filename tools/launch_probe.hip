@@ -1,5 +1,5 @@
 // tools/launch_probe.hip -- where a one-record GPU batch's ~18 us round trip
-// goes (dev tool, DESIGN.md section 7): median us of REPS calls of
+// goes (dev tool, DESIGN.md section 4.6): median us of REPS calls of
 //
 //   empty       an empty kernel, hipStreamSynchronize
 //   lds152      an empty kernel asking for 152 KiB of LDS (as the record kernels)

@@ -1,7 +1,7 @@
 // tools/route_probe.cc -- latency of one consus::crc32c call on host bytes,
 // through the GPU engine and through the engine's CPU path, by size (dev
 // tool; sets the size-routing default, include/consus_crc32c.h
-// mi_crc32c_set_gpu_min, DESIGN.md section 4.4).
+// mi_crc32c_set_gpu_min, DESIGN.md section 4.7).
 //
 //   route_probe [REPS]      prints one line per size: median us of each path
 //

@@ -1,4 +1,4 @@
-"""Piece path vs sorted path crossover (dev tool, DESIGN.md section 4.2 / 4.7).
+"""Piece path vs sorted path crossover (dev tool, DESIGN.md section 4.4 / 4.2).
 
 For batches of the configs[2] record stream (Zipf 64 B - 64 KiB, packed)
 cut to about 1 .. 256 MiB, times one batch call on each variable-length
