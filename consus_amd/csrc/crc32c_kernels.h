@@ -174,7 +174,7 @@ constexpr uint32_t kWinSmallCount = 768;  // ... and one wave per workgroup up t
 constexpr uint32_t kWinMaxCount = 8192;     // the engine's record bound (MI_CRC32C_WIN_MAX_COUNT: probes)
 constexpr uint32_t kWinBlockBig = 768;      // one workgroup per CU (12 waves) for batches that fill the CUs
 constexpr uint32_t kWinMaxCountBig = 16384; // the LDS prefix's bound (64 KiB)
-size_t window_lds_bytes(uint32_t count, uint32_t block);
+size_t window_lds_bytes(uint32_t count);
 uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_t block, uint32_t rows);
 hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint32_t* inits, uint64_t count, uint64_t total_bytes, uint32_t* out,

@@ -2464,12 +2464,6 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #ifndef MI_SORT_PREFETCH
 #define MI_SORT_PREFETCH 1
 #endif
-// A/B (round 6, VERDICT r5 Next 2b): rows per team of the first 32 groups
-// read with the default policy while the table image is staged (HBM is idle
-// in the prologue), so that the group loop finds them in L2 / MALL.  0: off.
-#ifndef MI_SORT_EARLY_ROWS
-#define MI_SORT_EARLY_ROWS 0
-#endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 // where each workgroup ran: HW_ID (cu, sh, se fields) and XCC_ID (round 6)
@@ -2755,36 +2749,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
         __syncthreads();
     }
-#if MI_SORT_EARLY_ROWS
-    // the first rows of the items of groups 2w and 2w + 1 (the first two
-    // grabs of the 16 waves take groups 0..31)
-    uint32_t early = 0;
-    uint4 er[2][MI_SORT_EARLY_ROWS];
-    if (staged)
-    {
-#pragma unroll
-        for (uint32_t h = 0; h < 2; ++h)
-        {
-            const uint32_t i = (2 * (threadIdx.x >> 6) + h) * 8 + ((threadIdx.x & 63u) >> 3);
-            const uint4 d = i < n_full + S.lane_base ? stage_lds[i] : make_uint4(0, 0, 0, 0);
-            const uint64_t ps = (uint64_t(d.x) | (uint64_t(d.y) << 32)) & ~uint64_t(kRowBytes - 1);
-            const uint32_t rows = sort_rows(d);
-#pragma unroll
-            for (uint32_t k = 0; k < MI_SORT_EARLY_ROWS; ++k)
-                er[h][k] = k < rows ? load16_edge(reinterpret_cast<const uint8_t*>(ps + k * kRowBytes + (threadIdx.x & 7u) * 16u))
-                                    : make_uint4(0, 0, 0, 0);
-        }
-    }
-#endif
     stage_tables(tables);  // ends with a barrier
-#if MI_SORT_EARLY_ROWS
-    if (staged)
-#pragma unroll
-        for (uint32_t h = 0; h < 2; ++h)
-#pragma unroll
-            for (uint32_t k = 0; k < MI_SORT_EARLY_ROWS; ++k) early ^= er[h][k].x ^ er[h][k].w;
-    if (early == 0x9E3779B9u && n_items == 0xFFFFFFFFu) out[0] = early;  // never: keeps the loads
-#endif
     SORT_STAMP(4);
     // team items first, lane items (positions n_long ..) after them
     const uint32_t n_long = n_full + S.lane_base;
@@ -3340,20 +3305,6 @@ uint64_t sorted_item_cap(uint64_t count, uint64_t total_bytes, uint32_t plog, in
 #ifndef MI_WIN_SKIP
 #define MI_WIN_SKIP 0  // A/B timing builds only (wrong CRCs): 1 no combine, 2 no lookups, 4 no fold
 #endif
-#ifndef MI_WIN_LDSTAB
-#define MI_WIN_LDSTAB 0  // A/B builds: bit 0 in-wave window shifts from LDS, bit 1 Z_{-m} from LDS
-#endif
-// LDS table sets of the one-per-CU form (round 6, VERDICT r5 Next 5): the
-// G^{2^k} sets k = 0..6 and Z_{-128} (the finish Z_{-m} = Z_{-128} o Z_{128-m},
-// zneg), then G^{128 R d} for d = 1, 2, 4 (the in-wave window shifts).  Each
-// set is 4 x 256 words; staged once per workgroup from L2.
-constexpr uint32_t kWinTabSets = 11;
-constexpr uint32_t kWinTabBytes = kWinTabSets * 4096;
-template <uint32_t B>
-constexpr bool win_lds_tabs()
-{
-    return (MI_WIN_LDSTAB & 3) && B == kWinBlockBig;
-}
 __device__ __forceinline__ uint32_t wave_min32(uint32_t x)
 {
 #pragma unroll
@@ -3386,41 +3337,9 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
     uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tables, const uint32_t* __restrict__ pow2,
     uint32_t* __restrict__ ctrl)
 {
-    // LDS: [table sets (one-per-CU form)], first task of each record, wave
-    // sums (64-bit, 8-B aligned)
-    constexpr bool LT = win_lds_tabs<B>();
-    constexpr uint32_t tab_bytes = LT ? kWinTabBytes : 0u;
-    uint32_t* const s_tab = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* const s_pre = reinterpret_cast<uint32_t*>(smem + tab_bytes);
-    uint64_t* const s_wsum = reinterpret_cast<uint64_t*>(smem + tab_bytes + ((size_t(count) * 4 + 7) & ~size_t(7)));
-    if constexpr (LT)
-    {
-        // every load issued before any store: one L2 round trip
-        constexpr uint32_t n4 = kWinTabSets * 256, per = (n4 + B - 1) / B;
-        constexpr uint32_t lg = R == 4 ? 9u : R == 8 ? 10u : 11u;  // log2(128 R)
-        uint4 v[per];
-#pragma unroll
-        for (uint32_t j = 0; j < per; ++j)
-        {
-            const uint32_t i = threadIdx.x + j * B;
-            const uint32_t set = i >> 8, w = (i & 255u) * 4u;
-            if (i < n4 && ((set < 8 && (MI_WIN_LDSTAB & 2)) || (set >= 8 && (MI_WIN_LDSTAB & 1))))
-            {
-                const uint32_t* src = set < 7   ? pow2 + set * 1024u
-                                      : set == 7 ? tables + kTabZInv128
-                                                 : pow2 + (lg + set - 8u) * 1024u;
-                v[j] = *reinterpret_cast<const uint4*>(src + w);
-            }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < per; ++j)
-        {
-            const uint32_t i = threadIdx.x + j * B;
-            const uint32_t set = i >> 8;
-            if (i < n4 && ((set < 8 && (MI_WIN_LDSTAB & 2)) || (set >= 8 && (MI_WIN_LDSTAB & 1))))
-                reinterpret_cast<uint4*>(s_tab)[i] = v[j];
-        }
-    }
+    // LDS: first task of each record, wave sums (64-bit, 8-B aligned)
+    uint32_t* const s_pre = reinterpret_cast<uint32_t*>(smem);
+    uint64_t* const s_wsum = reinterpret_cast<uint64_t*>(smem + ((size_t(count) * 4 + 7) & ~size_t(7)));
     LaneTabs lt;
     load_lane_tabs<6 * kLaneOps>(lt, tables);
     // (1) windows per record, from the lengths alone (an empty record: one
@@ -3562,61 +3481,25 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
                 U[q] = lo8;
         }
         const uint32_t W = team_fold_lane(U, lt);
+        // this window's value as of row Re (team leaders; 0 for no record)
+        uint32_t T = live && L ? W : 0u;
+        if (k && !(MI_WIN_SKIP & 2))
+        {
+            const uint32_t kb = k * (R / 4);  // shift in 512 B
+            T = kb < kWinShifts ? zglob(tables + kTabZWin + (kb - 1) * 1024u, T)
+                                : zshift48(pow2, T, uint64_t(k) * R * kRowBytes);
+        }
+        // XOR over this wave's windows of the same record
         const uint32_t rr = live ? r : 0xFFFFFFFFu;
         uint32_t seg = 0;
         bool lead = true;
-        if constexpr (LT)
-        {
-            // The windows of a record in this wave are consecutive teams, k
-            // falling by one from team to team.  A segmented scan over the
-            // teams (Z_{128 R d} from LDS, d = 1, 2, 4) leaves in the
-            // segment's last team XOR_i Z_{128 R (k_i - k)}(W_i); one shift
-            // Z_{128 R k} then moves it to row Re, and only for a segment that
-            // does not hold the record's last window (k > 0).  Round 5 took a
-            // global Z_{512 k} lookup per window (L2 misses in 8 L2s: most of
-            // the kernel's 1.2x over-fetch, profiles/r05_window_kernel_stats.txt).
-            seg = live && L ? W : 0u;
-            const int ln = int(threadIdx.x & 63u);
 #pragma unroll
-            for (uint32_t q = 0; q < 3; ++q)
-            {
-                const uint32_t d = 1u << q;
-                const int src = (ln - int(8 * d)) & 63;
-                const uint32_t rs = uint32_t(__shfl(int(rr), src));
-                const uint32_t as = uint32_t(__shfl(int(seg), src));
-                const uint32_t* zt = (MI_WIN_LDSTAB & 1) ? s_tab + (8u + q) * 1024u
-                                                         : pow2 + ((R == 4 ? 9u : R == 8 ? 10u : 11u) + q) * 1024u;
-                const uint32_t sh = (MI_WIN_SKIP & 2) ? as : zglob(zt, as);
-                if (tw >= d && rs == rr) seg ^= sh;
-            }
-            const uint32_t rn = uint32_t(__shfl(int(rr), (ln + 8) & 63));
-            lead = tw == 7 || rn != rr;
-            if (k && lead && !(MI_WIN_SKIP & 2))
-            {
-                const uint32_t kb = k * (R / 4);  // shift in 512 B
-                seg = kb < kWinShifts ? zglob(tables + kTabZWin + (kb - 1) * 1024u, seg)
-                                      : zshift48(pow2, seg, uint64_t(k) * R * kRowBytes);
-            }
-        }
-        else
+        for (uint32_t j = 0; j < 8; ++j)
         {
-            // this window's value as of row Re (team leaders; 0 for no record)
-            uint32_t T = live && L ? W : 0u;
-            if (k && !(MI_WIN_SKIP & 2))
-            {
-                const uint32_t kb = k * (R / 4);  // shift in 512 B
-                T = kb < kWinShifts ? zglob(tables + kTabZWin + (kb - 1) * 1024u, T)
-                                    : zshift48(pow2, T, uint64_t(k) * R * kRowBytes);
-            }
-            // XOR over this wave's windows of the same record
-#pragma unroll
-            for (uint32_t j = 0; j < 8; ++j)
-            {
-                const uint32_t rj = uint32_t(__shfl(int(rr), int(8 * j)));
-                const uint32_t Tj = uint32_t(__shfl(int(T), int(8 * j)));
-                seg ^= rj == rr ? Tj : 0u;
-                lead = lead && !(j < tw && rj == rr);
-            }
+            const uint32_t rj = uint32_t(__shfl(int(rr), int(8 * j)));
+            const uint32_t Tj = uint32_t(__shfl(int(T), int(8 * j)));
+            seg ^= rj == rr ? Tj : 0u;
+            lead = lead && !(j < tw && rj == rr);
         }
         if (tl == 0 && live && lead)
         {
@@ -3657,9 +3540,7 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
                 if (fin)
                 {
                     const uint32_t m = uint32_t(uint64_t(Re) * kRowBytes - E);
-                    uint32_t v = (MI_WIN_SKIP & 2) ? seg
-                                 : LT && (MI_WIN_LDSTAB & 2) ? zneg(s_tab, s_tab + 7 * 1024, seg, m)
-                                                   : zglob(tables + kTabZNeg + m * 1024u, seg);
+                    uint32_t v = (MI_WIN_SKIP & 2) ? seg : zglob(tables + kTabZNeg + m * 1024u, seg);
                     if (!with_init) v ^= zbits(tables + kTabP2, ninit, L);  // seed Z_L(~init)
                     out[r] = ~v;
                 }
@@ -3668,11 +3549,7 @@ __global__ __launch_bounds__(B) void crc32c_window_kernel(
     }
 }
 
-size_t window_lds_bytes(uint32_t count, uint32_t block)
-{
-    const bool lt = block == kWinBlockBig ? win_lds_tabs<kWinBlockBig>() : false;
-    return (lt ? kWinTabBytes : 0u) + ((size_t(count) * 4 + 7) & ~size_t(7)) + 8 * (kWinBlockBig / 64);
-}
+size_t window_lds_bytes(uint32_t count) { return ((size_t(count) * 4 + 7) & ~size_t(7)) + 8 * (kWinBlockBig / 64); }
 
 uint64_t window_grid(uint64_t count, uint64_t total_bytes, int grid_cap, uint32_t block, uint32_t rows)
 {
@@ -3723,7 +3600,7 @@ hipError_t launch_window(const void* base, const uint64_t* offsets, const uint32
                                      : (rows == 4   ? crc32c_window_kernel<kWinBlockMax, 4>
                                         : rows == 8 ? crc32c_window_kernel<kWinBlockMax, 8>
                                                     : crc32c_window_kernel<kWinBlockMax, 16>);
-    hipLaunchKernelGGL(k, dim3(g), dim3(block), window_lds_bytes(uint32_t(count), block), stream,
+    hipLaunchKernelGGL(k, dim3(g), dim3(block), window_lds_bytes(uint32_t(count)), stream,
                        static_cast<const uint8_t*>(base), offsets, lengths, inits, uint32_t(count),
                        out, acc64, acc, cnt, tables, pow2, ctrl);
     return hipGetLastError();
@@ -3766,7 +3643,7 @@ hipError_t configure_kernels()
     for (const void* f : kw)
         if (e == hipSuccess)
             e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    int(window_lds_bytes(kWinMaxCountBig, kWinBlockBig)));
+                                    int(window_lds_bytes(kWinMaxCountBig)));
     const void* ks[] = {reinterpret_cast<const void*>(&crc32c_sorted_kernel<2>),
                         reinterpret_cast<const void*>(&crc32c_sorted_kernel<4>)};
     for (const void* f : ks)
