@@ -154,6 +154,16 @@ while [ $# -gt 0 ]; do
                (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/wf_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --mib $m --reps 20 > "$OUT/wf_$m.log" 2>&1) || { tail -20 "$OUT/wf_$m.log"; exit 1; }
                echo "== $m MiB"; python3 tools/pmc_summary.py "$OUT/wf_$m" window_kernel; rm -rf "$OUT/wf_$m"
              done | tee "$OUT/winfetch.out" ;;
+    winattr) C="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+             for v in ${WINATTR_LIBS:-head winskip2 winskip7}; do
+               lib=tools/ab/libconsus_crc32c_$v.so; [ "$v" = head ] && lib=consus_amd/lib/libconsus_crc32c.so
+               for m in ${WIN_MIB:-16}; do
+                 (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/wa_${v}_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --lib "$ROOT/$lib" --path window --mib $m --reps 20 > "$OUT/wa_${v}_$m.log" 2>&1) || { tail -20 "$OUT/wa_${v}_$m.log"; exit 1; }
+                 echo "== $v $m MiB"; python3 tools/pmc_summary.py "$OUT/wa_${v}_$m" window_kernel; rm -rf "$OUT/wa_${v}_$m"
+                 (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/wb_${v}_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --lib "$ROOT/$lib" --path window --mib $m --reps 20 > "$OUT/wb_${v}_$m.log" 2>&1) || { tail -20 "$OUT/wb_${v}_$m.log"; exit 1; }
+                 python3 tools/pmc_summary.py "$OUT/wb_${v}_$m" window_kernel; rm -rf "$OUT/wb_${v}_$m"
+               done
+             done | tee "$OUT/winattr.out" ;;
     winprof) for m in ${WIN_MIB:-1 16 20}; do
                (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/wp_$m" -o k -- python3 "$ROOT/tools/mid_probe.py" --mib $m --reps 100 > "$OUT/wp_$m.log" 2>&1) || { tail -20 "$OUT/wp_$m.log"; exit 1; }
                find "$OUT/wp_$m" -name '*kernel_stats.csv' -exec cp {} "$OUT/window_${m}mib_kernel_stats.csv" \;
