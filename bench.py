@@ -1139,6 +1139,37 @@ def compact_line(rec: dict, detail: str | None) -> dict:
     return line
 
 
+def _clip_strings(x, n: int):
+    """Every string inside x cut to n characters (error texts, samples)."""
+    if isinstance(x, str):
+        return x if len(x) <= n else x[:n - 3] + "..."
+    if isinstance(x, dict):
+        return {k: _clip_strings(v, n) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_clip_strings(v, n) for v in x]
+    return x
+
+
+def fit_line(line: dict) -> dict:
+    """Keep the printed line under LINE_LIMIT whatever the legs carry (a
+    failing leg's error text, say): long strings are clipped first, then the
+    durable-log leg keeps only its headline ratios; configs[2] stays last."""
+    if len(json.dumps(line)) <= LINE_LIMIT:
+        return line
+    line = _clip_strings(line, 160)
+    if len(json.dumps(line)) > LINE_LIMIT and isinstance(line.get("durable_log"), dict):
+        d = line["durable_log"]
+        slim = {k: d[k] for k in ("value", "unit", "digest_verified", "error") if k in d}
+        slim.update({w: {"gpu_vs": v.get("gpu_vs")} for w, v in d.items()
+                     if isinstance(v, dict) and "gpu_vs" in v})
+        rest = {k: v for k, v in line.items() if k not in LEG_ORDER}
+        rest.update({k: (slim if k == "durable_log" else line[k]) for k in LEG_ORDER if k in line})
+        line = rest
+    if len(json.dumps(line)) > LINE_LIMIT:
+        line = _clip_strings(line, 60)
+    return line
+
+
 def write_detail(rec: dict) -> str | None:
     """The full record (every run, every sample string) to BENCH_DETAIL, by
     default gpurun_out/bench_detail.json; returns the path the line names."""
@@ -1393,7 +1424,7 @@ def main():
         gather = rccl_gather(E, dist, rank, world, out, R, digests, rec) if do_gather else None
         code = multi_rank_fields(rec, ranks, gather, world, args.share_device)
     if leg_res:
-        rec = compact_line(rec, write_detail(rec))
+        rec = fit_line(compact_line(rec, write_detail(rec)))
     print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -79,3 +79,22 @@ def test_compact_keeps_the_durable_log_comparison():
         assert e["gpu"][1] == round(src["durable_latency_us"]["p50_median"])
         assert set(d[w]["gpu_vs"]) == {"reference-scheme", "reference-cpu", "no-checksum"}
         assert "batch_crc" in d[w]["flush"]["us_per_flush"]
+
+
+def test_failing_legs_keep_the_line_under_the_limit():
+    """A leg that fails carries its error text; however long, the printed line
+    stays under the limit with configs[2] last (bench.fit_line)."""
+    import bench
+    with open(os.path.join(REPO, "profiles", "r05_bench_default_session_r05bs.json")) as f:
+        full = json.loads(f.read().strip().splitlines()[-1])
+    full["config4_stream"] = {"error": "Traceback (most recent call last):\n" + "x" * 8000}
+    full["durable_log"]["error"] = "y" * 5000
+    full["durable_log"]["workloads"]["zipf_sink"] = full["durable_log"]["workloads"]["zipf"]
+    line = bench.fit_line(bench.compact_line(full, "gpurun_out/bench_detail.json"))
+    text = json.dumps(line)
+    assert len(text.encode()) < bench.LINE_LIMIT
+    assert list(line)[-1] == "config2_zipf"
+    assert line["config2_zipf"]["ms_per_step"] == full["config2_zipf"]["ms_per_step"]
+    assert line["config4_stream"]["error"].startswith("Traceback")
+    for k in ("metric", "value", "roofline", "cpu_baseline"):
+        assert k in line
