@@ -1902,6 +1902,10 @@ constexpr uint32_t kSortMulti = 0x80000000u;  // descriptor flag: a piece of a s
 constexpr uint32_t kSortFirst = 0x40000000u;  // ... its first piece (carries the init)
 constexpr uint32_t kSortRecMask = 0x3FFFFFFFu;
 constexpr uint32_t kSortNone = 0xFFFFFFFFu;   // team without an item
+constexpr uint32_t kSortJJNone = 0xFFFFu;     // descriptor: the piece's E - pe not held (read off/len)
+#ifndef MI_SORT_JJ
+#define MI_SORT_JJ 1  // A/B builds: 0 = every piece's shift from off[] / len[] (round 5)
+#endif
 
 uint32_t sorted_blocks(uint64_t count) { return uint32_t((count + kSortRecs - 1) / kSortRecs); }
 
@@ -2250,11 +2254,18 @@ struct SortView
     uint32_t m;      // bytes masked after the item in the last row
     uint32_t recf;   // record | flags, kSortNone: no item
     uint32_t slot;   // the item's descriptor slot (whole records)
+    uint32_t jj;     // a piece's E - pe in pieces (kSortJJNone: not held)
 };
+
+
+__device__ __forceinline__ uint64_t sort_addr(const uint4& d)
+{
+    return uint64_t(d.x) | (uint64_t(d.y & 0xFFFFu) << 32);
+}
 
 __device__ __forceinline__ uint32_t sort_rows(const uint4& d)
 {
-    const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
+    const uint64_t ps = sort_addr(d);
     return d.z ? uint32_t(((ps + d.z + kRowBytes - 1) >> 7) - (ps >> 7)) : 0u;
 }
 
@@ -2284,8 +2295,9 @@ __device__ __forceinline__ SortView sort_view(const uint4& d, int32_t n, uint32_
     const int32_t se = s0 + int32_t(L);
     const int32_t rows = L ? (se + int32_t(kRowBytes) - 1) >> 7 : 0;
     v.recf = L ? d.w : kSortNone;
+    v.jj = d.y >> 16;
     v.f = n - rows;
-    const uint64_t ps = uint64_t(d.x) | (uint64_t(d.y) << 32);
+    const uint64_t ps = sort_addr(d);
     v.p0 = ps + int64_t(int32_t(uint32_t(rows - n) * kRowBytes + tl * 16u) - s0);
     const int32_t q = s0 - int32_t(tl) * 16;
     const int32_t bs = min(max(q, 0), 16);
@@ -2336,6 +2348,17 @@ __device__ __forceinline__ uint32_t zshift48(const uint32_t* __restrict__ pow2, 
     for (int k = 0; n && k < 48; ++k, n >>= 1)
         if (n & 1u) v = zglob(pow2 + k * 1024, v);
     return v;
+}
+
+// Z_{P jj}(v), a piece's shift to its record's end: one lookup in the Z_{512 k}
+// sets when P jj / 512 < 256 (4-16 KiB pieces of records up to 128 KiB),
+// else popcount lookups in the G^{2^k} sets.
+__device__ __forceinline__ uint32_t zshift_piece(const uint32_t* __restrict__ tables,
+                                                 const uint32_t* __restrict__ pow2, uint32_t v, uint64_t n)
+{
+    const uint64_t k = n >> 9;
+    if ((n & 511u) == 0 && k - 1 < uint64_t(kWinShifts - 1)) return zglob(tables + kTabZWin + (k - 1) * 1024u, v);
+    return zshift48(pow2, v, n);
 }
 
 // One-launch form (round 5, VERDICT r4 Next 1a): the work of
@@ -2608,7 +2631,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         const bool head = k + 1 == f.s.n;
         const uint64_t pe = E - (uint64_t(head ? f.s.n - 1 : f.s.n - 2 - k) << plog);
         const uint64_t ps = head ? a : pe - piece;
-        return make_uint4(uint32_t(ps), uint32_t(ps >> 32), uint32_t(pe - ps),
+        // a piece's E - pe = P jj: jj in the top 16 bits of the address word
+        // (addresses are < 2^48), so its shift needs no off/len reads (kSortJJNone: read them)
+        const uint64_t jj = (E - pe) >> plog;
+        const uint32_t jw = f.s.n > 1 && MI_SORT_JJ ? uint32_t(min(jj, uint64_t(kSortJJNone))) << 16
+                                                    : uint32_t(kSortJJNone) << 16;
+        return make_uint4(uint32_t(ps), uint32_t(ps >> 32) | jw, uint32_t(pe - ps),
                           uint32_t(r) | (f.s.n > 1 ? kSortMulti : 0u) | (head ? kSortFirst : 0u));
     };
     uint4* const fullv = items + count;
@@ -2772,6 +2800,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     uint32_t pz = 0;               // this lane's Z_{-m} entry of the pending piece
     uint32_t p_recf = kSortNone;   // the pending piece's record | flags
     uint64_t p_pe = 0;             // its end (lane 0)
+    uint32_t p_jj = kSortJJNone;   // its E - pe in pieces (kSortJJNone: from off/len)
     bool p_multi = false;          // wave-uniform: some team has a pending piece
     auto flush = [&]() {
         if (!p_multi) return;
@@ -2782,9 +2811,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
         {
             // this piece's part: Z_{E - pe}(raw(piece)), E the record's end
             const uint32_t rec = p_recf & kSortRecMask;
-            const uint64_t a_rec = uint64_t(base) + off[rec];
-            const uint32_t L_rec = len[rec];
-            v = zshift48(pow2, v, a_rec + L_rec - p_pe);
+            if (p_jj != kSortJJNone)
+            {
+                // E - pe from the descriptor: no dependent off/len reads
+                if (p_jj) v = zshift_piece(tables, pow2, v, uint64_t(p_jj) << plog);
+            }
+            else
+            {
+                const uint64_t a_rec = uint64_t(base) + off[rec];
+                const uint32_t L_rec = len[rec];
+                v = zshift48(pow2, v, a_rec + L_rec - p_pe);
+            }
             __hip_atomic_fetch_xor(out + rec, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
@@ -2875,7 +2912,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             const uint32_t c1 = grab64();
             const uint4 d1 = ldesc(c1);
             const bool act = c0 + lane < n_lane;
-            const uint64_t a = uint64_t(d.x) | (uint64_t(d.y) << 32);
+            const uint64_t a = sort_addr(d);
             const uint64_t e = a + d.z;
             const uint32_t q = uint32_t(a) & 15u;
             const int32_t K = act ? int32_t(((e + 15) >> 4) - (a >> 4)) : 0;  // blocks, >= 1
@@ -2946,9 +2983,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
                 else
                 {
                     // the head of a split record: Z_{E - pe}(raw(head)), E the record's end
-                    const uint64_t E = uint64_t(base) + off[rec] + len[rec];
-                    __hip_atomic_fetch_xor(out + rec, zshift48(pow2, st, E - e), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t jj = d.y >> 16;
+                    const uint64_t sh = jj != kSortJJNone ? uint64_t(jj) << plog
+                                                          : uint64_t(base) + off[rec] + len[rec] - e;
+                    __hip_atomic_fetch_xor(out + rec, jj != kSortJJNone ? zshift_piece(tables, pow2, st, sh)
+                                                                        : zshift48(pow2, st, sh),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             c0 = c1;
@@ -3108,6 +3148,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             }
             p_recf = multi ? cur.recf : kSortNone;
             p_pe = cur.p0 + uint64_t(n) * kRowBytes - cur.m;
+            p_jj = cur.jj;
         }
         g_nxt = g_nn;
         d_nxt = d_nn;
@@ -3170,7 +3211,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
         {
-            const uint64_t ps = uint64_t(dv[u].x) | (uint64_t(dv[u].y) << 32);
+            const uint64_t ps = sort_addr(dv[u]);
             const uint32_t m = uint32_t(0u - uint32_t(ps + dv[u].z)) & 127u;
             uint32_t v = wv[u];
             const uint32_t n = 128u - m;
@@ -3203,7 +3244,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < FU; ++u)
         {
-            const uint64_t ps = uint64_t(dv[u].x) | (uint64_t(dv[u].y) << 32);
+            const uint64_t ps = sort_addr(dv[u]);
             const uint32_t m = uint32_t(0u - uint32_t(ps + dv[u].z)) & 127u;
             uint32_t v = wv[u];
             const uint32_t n = 128u - m;

@@ -64,6 +64,13 @@ if last == 7:
     fin = us[:, :, 7].max(axis=1) - us[:, :, 6].max(axis=1)
     print(f"finish pass per workgroup (after its last lane wave): median {np.median(fin):.2f} "
           f"max {fin.max():.2f}")
+# within one workgroup: how far apart its waves finish their team groups
+# (each wave takes groups from the workgroup's LDS counter, largest first)
+intra = us[:, :, 5].max(axis=1) - us[:, :, 5].min(axis=1)
+idle = (us[:, :, 5].max(axis=1)[:, None] - us[:, :, 5]).mean(axis=1)
+print(f"team-phase end spread within a workgroup (last - first wave): median {np.median(intra):.2f} "
+      f"max {intra.max():.2f}; mean wave wait for its workgroup's last wave: median {np.median(idle):.2f} "
+      f"max {idle.max():.2f}")
 print("per XCD group (workgroup % 8): median workgroup end " +
       " ".join(f"{np.median(wg_end[x::8]):.1f}" for x in range(8)))
 
