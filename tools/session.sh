@@ -66,6 +66,7 @@ while [ $# -gt 0 ]; do
               echo "round $rnd $eng $(cat "$OUT/dl.out")"
             done; done > "$OUT/dlogtl.out"; rm -rf /dev/shm/dltl; cut -c1-200 "$OUT/dlogtl.out" ;;
     sortedtests) run pytest_sorted 900 python -u -m pytest tests/test_gpu_sorted.py tests/test_gpu_fuzz.py tests/test_gpu_errors.py -x -q --timeout 300 --timeout-method thread ;;
+    soak) FUZZ_ROUNDS=${SOAK_ROUNDS:-1000} run fuzz_soak 900 python -u -m pytest tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     route) run route_probe 300 ./tools/route_probe 200 ;;
     flush) run flush_probe 300 ./tools/flush_probe 1000 ;;
