@@ -224,6 +224,29 @@ def test_sorted_one_huge_record(engine, oracle, sorted_path):
                           oracle.batch(buf, offsets, lengths, inits))
 
 
+@pytest.mark.parametrize("plog", ["9", "12", "14"])
+def test_sorted_piece_shift_forms(engine, oracle, plog, monkeypatch):
+    """Round 6: a piece's shift to its record's end, P jj, comes from its
+    descriptor (jj in the address word's top 16 bits): one Z_{512 k} lookup
+    while P jj / 512 < 256, the G^{2^k} chain beyond, and off/len re-read
+    when jj does not fit 16 bits.  A 40 MiB record cut into 512 B pieces has
+    81,920 of them (jj up to 81,919: all three forms); 4 and 16 KiB pieces
+    take the first two.  Records of 64-300 KiB beside
+    it, with inits."""
+    monkeypatch.setenv("MI_CRC32C_VARPATH", "sorted")
+    monkeypatch.setenv("MI_CRC32C_SORT_PIECE_LOG2", plog)
+    rng = np.random.default_rng(int(plog))
+    lengths = np.array([40 << 20, 65 << 10, 300 << 10, 129 << 10, 7, 100, 513, 2049],
+                       dtype=np.uint32)
+    offsets, end = _packed(rng, lengths, start=int(rng.integers(0, 128)))
+    buf = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    inits = rng.integers(0, 2**32, lengths.size, dtype=np.uint32)
+    before = engine.stats()["sorted_batches"]
+    assert np.array_equal(_device_run(engine, buf, offsets, lengths, inits),
+                          oracle.batch(buf, offsets, lengths, inits))
+    assert engine.stats()["sorted_batches"] > before
+
+
 @pytest.mark.parametrize("count", [1, 2, 7, 8, 9, 255, 257, 4097])
 def test_sorted_few_records(engine, oracle, sorted_path, count):
     """Fewer records than workgroups (most ranges empty) and partial groups."""
