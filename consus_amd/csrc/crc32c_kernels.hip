@@ -2487,6 +2487,12 @@ __device__ __forceinline__ bool sorted_fused_costs(const uint8_t* base, const ui
 #ifndef MI_SORT_PREFETCH
 #define MI_SORT_PREFETCH 1
 #endif
+// Timing ablation (dev builds only, wrong CRCs for the records it skips):
+// MI_SORT_ABL_LANE=1 leaves the lane items unhashed, to bound what any faster
+// lane phase could return (profiles/r06_lane_phase_ablation.txt).
+#ifndef MI_SORT_ABL_LANE
+#define MI_SORT_ABL_LANE 0
+#endif
 #if MI_SORT_STAMP
 __device__ uint64_t g_sort_stamp[256 * 16 * 8];
 // where each workgroup ran: HW_ID (cu, sh, se fields) and XCC_ID (round 6)
@@ -2888,6 +2894,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     // longer item takes another round)
     constexpr int32_t kLaneBlocks = MI_SORT_LANE_BLOCKS;
     auto lane_items = [&]() {
+        if (MI_SORT_ABL_LANE) return;
         const uint32_t n_lane = n_items - n_long;
         const uint4* const listLane = listL + n_long;
         auto grab64 = [&]() {
