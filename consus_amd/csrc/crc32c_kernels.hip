@@ -49,43 +49,60 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 // T_0..T_15, G^{32}, G^{64} verbatim.  Byte address of G^{128}_t[b] for the
 // lane whose ds_read_b32 group position is c (= lane & 31):
 //   (t >> 1) * 65536 + b * 256 + (t & 1) * 128 + c * 4   ->  bank == c.
-__device__ __forceinline__ void stage_tables(const uint32_t* __restrict__ g)
+// Every record kernel runs kBlock threads: all loads are issued first, then
+// all stores (one L2 round trip per thread, not one per iteration).  The two
+// halves are separate so that a kernel can issue the loads early and store
+// later (the sorted kernel: its LDS holds the descriptor list until then).
+struct TableRegs
 {
-    // Every record kernel runs kBlock threads: all loads are issued first,
-    // then all stores (one L2 round trip per thread, not one per iteration).
-    constexpr uint32_t NM = 1024u * 8u / kBlock;          // G^{128} entries x 8 quads
-    constexpr uint32_t NT = (4096u + 2048u) / 4u;         // T_0..15, G^32, G^64 as uint4
-    constexpr uint32_t NTI = (NT + kBlock - 1) / kBlock;
-    static_assert(1024u * 8u % kBlock == 0, "table staging shape");
+    static constexpr uint32_t NM = 1024u * 8u / kBlock;   // G^{128} entries x 8 quads
+    static constexpr uint32_t NT = (4096u + 2048u) / 4u;  // T_0..15, G^32, G^64 as uint4
+    static constexpr uint32_t NTI = (NT + kBlock - 1) / kBlock;
     uint32_t v[NM];
     uint4 t[NTI];
+};
+static_assert(1024u * 8u % kBlock == 0, "table staging shape");
+
+__device__ __forceinline__ void stage_tables_load(TableRegs& r, const uint32_t* __restrict__ g)
+{
     const uint4* src = reinterpret_cast<const uint4*>(g + kTabT);
 #pragma unroll
-    for (uint32_t k = 0; k < NM; ++k) v[k] = g[kTabMain + ((threadIdx.x + k * kBlock) >> 3)];
+    for (uint32_t k = 0; k < TableRegs::NM; ++k) r.v[k] = g[kTabMain + ((threadIdx.x + k * kBlock) >> 3)];
 #pragma unroll
-    for (uint32_t k = 0; k < NTI; ++k)
+    for (uint32_t k = 0; k < TableRegs::NTI; ++k)
     {
         const uint32_t i = threadIdx.x + k * kBlock;
-        t[k] = i < NT ? src[i] : make_uint4(0, 0, 0, 0);
+        r.t[k] = i < TableRegs::NT ? src[i] : make_uint4(0, 0, 0, 0);
     }
+}
+
+__device__ __forceinline__ void stage_tables_store(const TableRegs& r)
+{
 #pragma unroll
-    for (uint32_t k = 0; k < NM; ++k)
+    for (uint32_t k = 0; k < TableRegs::NM; ++k)
     {
         const uint32_t i = threadIdx.x + k * kBlock;
         const uint32_t e = i >> 3;          // t * 256 + b
         const uint32_t c4 = (i & 7u) * 4u;  // first of 4 consecutive copies
         const uint32_t tb = e >> 8, b = e & 255u;
         const uint32_t addr = (tb >> 1) * 65536u + b * 256u + (tb & 1u) * 128u + c4 * 4u;
-        *reinterpret_cast<uint4*>(smem + kLdsMain + addr) = make_uint4(v[k], v[k], v[k], v[k]);
+        *reinterpret_cast<uint4*>(smem + kLdsMain + addr) = make_uint4(r.v[k], r.v[k], r.v[k], r.v[k]);
     }
     uint4* dst = reinterpret_cast<uint4*>(smem + kLdsT);
 #pragma unroll
-    for (uint32_t k = 0; k < NTI; ++k)
+    for (uint32_t k = 0; k < TableRegs::NTI; ++k)
     {
         const uint32_t i = threadIdx.x + k * kBlock;
-        if (i < NT) dst[i] = t[k];
+        if (i < TableRegs::NT) dst[i] = r.t[k];
     }
     __syncthreads();
+}
+
+__device__ __forceinline__ void stage_tables(const uint32_t* __restrict__ g)
+{
+    TableRegs r;
+    stage_tables_load(r, g);
+    stage_tables_store(r);
 }
 
 // Lane info for the v_perm address builder: byte0 = c*4, byte1 = c*4 + 128,
@@ -2538,9 +2555,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     constexpr bool INLOOP = RB >= 4;
     if (INLOOP || MI_SORT_FIN_OVERLAP) S.zinv[threadIdx.x] = tables[kTabZInv128 + threadIdx.x];
     // (1) Wave 0: the two targets and the cost blocks holding them.  (The
-    // tables are staged later, at the stage_tables() call after the binning
-    // has written the descriptor list out: until then their LDS holds the
-    // list, so no table lookup may come before that call.)
+    // tables reach the LDS later, at the stage_tables_store() call after the
+    // binning has written the descriptor list out: until then their LDS holds
+    // the list, so no table lookup may come before that call.)
     SORT_STAMP(0);
 #if MI_SORT_STAMP
     if (threadIdx.x == 0 && blockIdx.x < 256)
@@ -2715,6 +2732,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
     pass(false);
     __syncthreads();
     SORT_STAMP(3);
+    // (round 6) The table image's global loads go out now, beside the bin
+    // scan, the placement and the list's copy-out; they reach the LDS once
+    // the list has left it (32 / 64 MiB batches 0.4-0.8 us faster, configs[2]
+    // unchanged: profiles/r06_early_table_loads_ab.txt)
+    TableRegs tregs;
+    stage_tables_load(tregs, tables);
     {
         const uint32_t c = threadIdx.x < kSortBins ? S.bins[threadIdx.x] : 0u;
         uint64_t total;
@@ -2783,7 +2806,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32c_sorted_kernel(
             put(i < n_full ? fullv + S.full_base + i : lastv + (i - n_full), stage_lds[i]);
         __syncthreads();
     }
-    stage_tables(tables);  // ends with a barrier
+    stage_tables_store(tregs);  // ends with a barrier
     SORT_STAMP(4);
     // team items first, lane items (positions n_long ..) after them
     const uint32_t n_long = n_full + S.lane_base;
