@@ -2,6 +2,8 @@
 # Whole lane records hashed by the cost kernel (default) or as lane items of
 # the hash kernel (MI_CRC32C_SORT_COST_LANES=0), interleaved on one box:
 # configs[2] (zipf_probe) and the mid-size batches (mid_probe).  Dev tool, round 6.
+# The knob belonged to the A/B build recorded in profiles/r06_lane_phase_ablation.txt
+# (2); that form was not kept, so on the product both settings run the same code.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 9
 OUT=gpurun_out/${SESSION:-r06zi}; mkdir -p "$OUT"

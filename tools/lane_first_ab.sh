@@ -1,7 +1,8 @@
 #!/bin/bash
 # Lane items before the team groups (MI_SORT_LANE_FIRST=1: every wave; 2: odd
 # waves) against after them (the product), interleaved on one box: configs[2]
-# (tools/ab.py --zipf) and the mid-size batches (mid_probe).  Dev tool, round 6.
+# (tools/ab.py --zipf) and the mid-size batches (mid_probe).  Dev tool, round 6;
+# LF_LIBS names any variant builds (tools/build_variant.sh) to compare the same way.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 9
 OUT=gpurun_out/${SESSION:-r06zj}; mkdir -p "$OUT"
